@@ -1,0 +1,209 @@
+"""Benchmark: Mray-steps/s (+ frames/s) of the neural-SDF sphere tracer at 1024^2 on plane_1.h5.
+
+BASELINE.json metric "Mray-steps/s + frames/s at 1024^2, plane_1.h5, 1/2/4/8 MI355X";
+workload = configs[1]: plane_1.h5, 1024x1024, 128 march steps, fp32, Chrome.png matcap,
+default camera (rx = ry = 0, zoom 2, frame 0), v1 scene (sceneSDF -> manySphere,
+volumeRender_kernel.cu:222).  One "step" = one frame rendered to device memory.
+
+    python bench.py [--gpus N --steps K --warmup W]
+N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt in 8-row
+bands round-robin (nr_render_shard), each rank renders its bands, one RCCL gather
+(torch.distributed.gather over the "nccl" backend) brings them to rank 0, which
+re-interleaves them (nr_assemble_shards).  The frame size is fixed as N grows:
+scaling "strong".
+
+Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
+k_march, f32 MFMA bound, per-launch HIP events on the stream it runs on) and
+`cpu_baseline` (the C oracle on the host cores, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FLOP_PER_EVAL = 2 * (3 * 32 + 7 * 32 * 32 + 32 * 1)   # 14,592
+PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}  # TFLOP/s dense, MI355X_MICROARCH.md
+W = H = 1024
+MAX_STEPS = 128
+BAND = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
+    ap.add_argument("--geometry", default="plane_1")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def cpu_baseline(size, max_steps, threads, geometry, matcap, iv, nm):
+    """C oracle (oracle/nr_oracle.c, OpenMP over rays) on the host cores.
+
+    Sample: one full frame of the benchmark workload when it fits the 10-30 s budget,
+    else a 512^2 frame of the same camera/steps."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    import cudaneuralrender_amd as nr
+    dims, K, B = nr.read_keras_h5(nr.geometry_path(geometry))
+    net = oracle.OracleNet(K, B)
+    # calibrate on a 256^2 frame, then pick the sample
+    t0 = time.perf_counter()
+    _, st = net.render(256, 256, iv, nm, color_type=1, matcap=matcap, max_steps=max_steps, nthreads=threads)
+    rate = st["ray_steps"] / (time.perf_counter() - t0)
+    est_full = 15e6 * (size / 1024) ** 2 / max(rate, 1.0)
+    s = size if est_full <= 30.0 else 512
+    t0 = time.perf_counter()
+    _, st = net.render(s, s, iv, nm, color_type=1, matcap=matcap, max_steps=max_steps, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(st["ray_steps"] / dt / 1e6, 4), "unit": "Mray-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{geometry} {s}x{s}, {max_steps} steps, Chrome matcap, default camera: "
+                      f"{st['ray_steps']} ray-steps in {dt:.2f} s (C oracle, OpenMP, {threads} threads, "
+                      f"host {os.cpu_count()} logical CPUs)"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import cudaneuralrender_amd as nr
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    size = a.size
+    r = nr.Renderer(local)
+    r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
+    iv, nm = nr.camera(0.0, 0.0, 2.0)
+    matcap = nr.load_png(nr.matcap_path("Chrome"))
+    r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
+    stream = torch.cuda.current_stream()
+    r.set_stream(stream.cuda_stream)
+
+    rows = nr.shard_rows(size, BAND, world, rank)
+    max_rows = max(nr.shard_rows(size, BAND, world, s) for s in range(world))
+    shard_buf = torch.zeros(max_rows * size, dtype=torch.int32, device="cuda")
+    gather_buf = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if rank == 0 else None
+    frame = torch.zeros(size * size, dtype=torch.int32, device="cuda") if rank == 0 else None
+
+    def step():
+        if world == 1:
+            r.render_device(frame.data_ptr(), size, size, a.max_steps)
+            return
+        r.render_shard_device(shard_buf.data_ptr(), size, size, BAND, world, rank, a.max_steps)
+        dist.gather(shard_buf, list(gather_buf.unbind(0)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            r.assemble_device(gather_buf.data_ptr(), max_rows * size, frame.data_ptr(), size, size, BAND, world)
+
+    # work per frame (deterministic): ray-steps of this rank's shard, summed over ranks
+    st = r.render_shard(size, size, BAND, world, rank, a.max_steps)[1]
+    steps_t = torch.tensor([st["ray_steps"], st["shade_evals"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(steps_t)
+    ray_steps, shade_evals = (float(v) for v in steps_t.tolist())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    r.prof_collect()          # drop anything recorded so far
+    r.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    r.set_profiling(False)
+    prof = r.prof_collect()
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    # parity spot-check of the timed output (outside the timed region)
+    parity = None
+    if rank == 0:
+        ref = r.render(size, size, a.max_steps, with_stats=False)
+        got = frame.cpu().numpy().view(np.uint32).reshape(size, size)
+        parity = bool(np.array_equal(ref, got))
+
+    # roofline of the dominant kernel (k_march) from this rank's per-launch events
+    march_avg_ms = prof["march_ms"] / max(prof["march_launches"], 1)
+    local_steps = st["ray_steps"] * prof["renders"]
+    flop_per_launch = local_steps * FLOP_PER_EVAL / max(prof["march_launches"], 1)
+    achieved = flop_per_launch / (march_avg_ms * 1e-3) / 1e12 if march_avg_ms > 0 else 0.0
+    peak = PEAK[a.precision]
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = ray_steps * a.steps / dt / 1e6
+    out = {
+        "metric": "Mray-steps/s at 1024^2, plane_1.h5 (frames/s in config.fps)",
+        "value": round(value, 3),
+        "unit": "Mray-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32" if a.precision == "fp32" else a.precision,
+        "data": "synthetic camera (default pose), real bundled weights plane_1.h5 + Chrome.png",
+        "config": {
+            "workload": f"{a.geometry} {size}x{size}, {a.max_steps} march steps, {a.precision}, Chrome.png, "
+                        "v1 scene, default camera (BASELINE configs[1])",
+            "fps": round(a.steps / dt, 3),
+            "ray_steps_per_frame": int(ray_steps),
+            "shade_evals_per_frame": int(shade_evals),
+            "parallelism": f"row-band shards x{world} + RCCL gather" if world > 1 else "single GPU",
+            "parity_vs_single_gpu_render": parity,
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "k_march",
+            "achieved": round(achieved, 3),
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": None,
+            "flop_per_launch": round(flop_per_launch, 1),
+            "avg_launch_ms": round(march_avg_ms, 5),
+            "launches": int(prof["march_launches"]),
+            "shade_ms_per_frame": round(prof["shade_ms"] / max(prof["renders"], 1), 4),
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(size, a.max_steps, a.cpu_threads, a.geometry, matcap, iv, nm)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+"""ctypes binding of libnr.so (C ABI: include/neural_render.h).
+
+The shared library is built in-tree (``make -C cudaneuralrender_amd/csrc``, or
+``__graft_entry__.build()``) into ``cudaneuralrender_amd/lib/libnr.so``.  There is
+no fallback: if the library is missing, importing the compute API raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnr.so")
+
+NR_OK = 0
+NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}
+NR_SCENE = {"v1": 0, "tanh": 1}
+NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
+NR_HOST, NR_DEVICE = 0, 1
+
+# every symbol include/neural_render.h declares
+EXPORTS = [
+    "nr_create", "nr_destroy", "nr_last_error", "nr_abi_version", "nr_set_stream", "nr_synchronize",
+    "nr_load_h5", "nr_load_mlp", "nr_mlp_info", "nr_set_precision", "nr_set_view", "nr_set_static",
+    "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_shard_rows",
+    "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
+    "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
+    "nr_set_poll_interval",
+]
+
+
+class NRStats(ctypes.Structure):
+    _fields_ = [
+        ("ray_steps", ctypes.c_uint64),
+        ("shade_evals", ctypes.c_uint64),
+        ("rays_hit", ctypes.c_uint64),
+        ("rays_shaded", ctypes.c_uint64),
+        ("iterations", ctypes.c_int32),
+        ("launches", ctypes.c_int32),
+        ("ms_total", ctypes.c_float),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class NRKernelProf(ctypes.Structure):
+    _fields_ = [
+        ("march_ms", ctypes.c_double),
+        ("shade_ms", ctypes.c_double),
+        ("init_ms", ctypes.c_double),
+        ("march_launches", ctypes.c_uint64),
+        ("shade_launches", ctypes.c_uint64),
+        ("init_launches", ctypes.c_uint64),
+        ("renders", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class NRError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[nr error {code}] {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib():
+    """Load libnr.so (once).  Raises if the HIP extension has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libnr.so not built: {LIB_PATH} missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, F, L64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
+    FP = ctypes.POINTER(ctypes.c_float)
+    IP = ctypes.POINTER(ctypes.c_int)
+    sig = {
+        "nr_create": (I, [I, ctypes.POINTER(P)]),
+        "nr_destroy": (I, [P]),
+        "nr_last_error": (ctypes.c_char_p, [P]),
+        "nr_abi_version": (I, []),
+        "nr_set_stream": (I, [P, P]),
+        "nr_synchronize": (I, [P]),
+        "nr_load_h5": (I, [P, ctypes.c_char_p]),
+        "nr_load_mlp": (I, [P, I, IP, ctypes.POINTER(FP), ctypes.POINTER(FP)]),
+        "nr_mlp_info": (I, [P, IP, IP, IP, IP]),
+        "nr_set_precision": (I, [P, I]),
+        "nr_set_view": (I, [P, FP, FP, I]),
+        "nr_set_static": (I, [P, I, I]),
+        "nr_set_scene": (I, [P, I]),
+        "nr_set_matcap": (I, [P, P, I, I]),
+        "nr_render": (I, [P, P, I, I, I, I, ctypes.POINTER(NRStats)]),
+        "nr_render_shard": (I, [P, P, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
+        "nr_shard_rows": (I, [I, I, I, I]),
+        "nr_assemble_shards": (I, [P, P, ctypes.c_size_t, P, I, I, I, I, I]),
+        "nr_mlp_forward": (I, [P, P, P, L64, I]),
+        "nr_layer_forward": (I, [P, I, P, P, L64, I]),
+        "nr_camera": (I, [F, F, F, F, F, FP, FP]),
+        "nr_h5_read_keras": (I, [ctypes.c_char_p, I, IP, IP, FP, ctypes.c_size_t]),
+        "nr_png_load": (I, [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)), IP, IP]),
+        "nr_png_save": (I, [ctypes.c_char_p, P, I, I, I]),
+        "nr_ppm_save": (I, [ctypes.c_char_p, P, I, I]),
+        "nr_free": (None, [P]),
+        "nr_set_profiling": (I, [P, I]),
+        "nr_prof_collect": (I, [P, ctypes.POINTER(NRKernelProf)]),
+        "nr_set_poll_interval": (I, [P, I]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc, ctx=None):
+    if rc != NR_OK:
+        msg = lib().nr_last_error(ctx)
+        raise NRError(rc, msg.decode() if msg else "")
+    return rc

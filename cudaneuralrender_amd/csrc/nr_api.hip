@@ -1,0 +1,646 @@
+// nr_api.hip -- the C ABI of libnr.so (include/neural_render.h): contexts, buffers,
+// the render loop driver and the host helpers.
+//
+// Replaces, on the reference side (daviesthomas/cudaNeuralRender @ v1):
+//   render_kernel / copyViewMatrices / copyStaticSettings  src/volumeRender_kernel.cu:608-706
+//   allocateBuffers + the static scratch globals           :578-606
+//   NeuralNetwork::load / forward                          src/neuralNetwork.cpp:54-151
+//   DenseLayer ctor / forward                              src/layers/denseLayer.cu:180-278
+//   Image::loadPNG / savePNG                               src/neuralUtils/image.cu:36-110
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "nr_internal.h"
+#include "nr_kernels.h"
+
+using namespace nr;
+
+struct nr_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+
+    // network
+    std::vector<int> dims;
+    std::vector<std::vector<float>> kernels, biases;  // Keras (in x out), bias
+    std::vector<float *> d_W, d_b;                     // out-major per layer (generic kernel)
+    bool fused = false;
+    int precision = NR_PRECISION_FP32;
+    float *d_pack32 = nullptr;
+    uint16_t *d_lp = nullptr;
+    float *d_lpf = nullptr;
+    MlpArgs mlp{};
+
+    // settings
+    float inv_view[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 2};
+    float normal[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, -2, 0, 0, 0, 1};
+    int frame = 0, color_type = NR_COLOR_FACING, num_inputs = 3, scene = NR_SCENE_V1;
+    uint32_t *d_matcap = nullptr;
+    int mw = 0, mh = 0;
+
+    // scratch (owned per context; the reference keeps static globals)
+    size_t cap_rays = 0;
+    float4 *d_P[2] = {nullptr, nullptr}, *d_D[2] = {nullptr, nullptr};
+    float4 *d_SP = nullptr, *d_SD = nullptr;
+    size_t cap_ctr = 0;
+    uint32_t *d_ctr = nullptr;       // [cap_ctr]: live counts per iteration, then shade count, then shade_it
+    uint32_t *h_ctr = nullptr;       // pinned mirror
+    size_t cap_out = 0;
+    uint32_t *d_out = nullptr;
+    size_t cap_io = 0;
+    float *d_io = nullptr;           // mlp_forward staging
+    int check_every = 32;            // host polls the live count every N iterations
+
+    // per-launch profiling (nr_set_profiling)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    struct Rec { int kind; int e0, e1; };   // kind 0 init, 1 march, 2 shade
+    std::vector<Rec> recs;
+    uint64_t prof_renders = 0;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int set_err(nr_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                            \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) return set_err(ctx, NR_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+void dfree(T *&p) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+}
+
+int free_network(nr_ctx *c) {
+    for (auto *p : c->d_W) (void)hipFree(p);
+    for (auto *p : c->d_b) (void)hipFree(p);
+    c->d_W.clear(); c->d_b.clear();
+    dfree(c->d_pack32); dfree(c->d_lp); dfree(c->d_lpf);
+    c->fused = false;
+    return NR_OK;
+}
+
+int upload_lowp(nr_ctx *c) {
+    dfree(c->d_lp); dfree(c->d_lpf);
+    c->mlp.lp = nullptr; c->mlp.lpf = nullptr; c->mlp.lp_bytes = 0; c->mlp.lpf_bytes = 0;
+    if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
+    std::vector<uint16_t> a;
+    std::vector<float> f;
+    if (!pack_lowp(c->dims, c->kernels, c->biases, c->precision, a, f))
+        return set_err(c, NR_E_INVALID, "low-precision pack failed");
+    size_t ab = (a.size() * 2 + 15) / 16 * 16, fb = (f.size() * 4 + 15) / 16 * 16;
+    a.resize(ab / 2, 0); f.resize(fb / 4, 0.0f);
+    HIPCHK(c, hipMalloc(&c->d_lp, ab));
+    HIPCHK(c, hipMalloc(&c->d_lpf, fb));
+    HIPCHK(c, hipMemcpy(c->d_lp, a.data(), ab, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_lpf, f.data(), fb, hipMemcpyHostToDevice));
+    c->mlp.lp = c->d_lp; c->mlp.lpf = c->d_lpf;
+    c->mlp.lp_bytes = (int)ab; c->mlp.lpf_bytes = (int)fb;
+    return NR_OK;
+}
+
+int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>> K, std::vector<std::vector<float>> B) {
+    HIPCHK(c, hipSetDevice(c->device));
+    free_network(c);
+    c->dims = std::move(dims); c->kernels = std::move(K); c->biases = std::move(B);
+    int nl = (int)c->dims.size() - 1;
+    for (int l = 0; l < nl; ++l) {
+        int in = c->dims[l], out = c->dims[l + 1];
+        // DenseLayer::initializeWeights (denseLayer.cu:217-227): W[y*in + x] = kernel[x][y]
+        std::vector<float> W((size_t)in * out);
+        for (int x = 0; x < in; ++x)
+            for (int y = 0; y < out; ++y) W[(size_t)y * in + x] = c->kernels[l][(size_t)x * out + y];
+        float *dw = nullptr, *db = nullptr;
+        HIPCHK(c, hipMalloc(&dw, W.size() * 4));
+        HIPCHK(c, hipMalloc(&db, (size_t)out * 4));
+        c->d_W.push_back(dw); c->d_b.push_back(db);
+        HIPCHK(c, hipMemcpy(dw, W.data(), W.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(db, c->biases[l].data(), (size_t)out * 4, hipMemcpyHostToDevice));
+    }
+    std::vector<float> pack;
+    c->fused = pack_fp32(c->dims, c->kernels, c->biases, pack);
+    c->mlp = MlpArgs{};
+    if (c->fused) {
+        size_t pb = (pack.size() * 4 + 15) / 16 * 16;
+        pack.resize(pb / 4, 0.0f);
+        HIPCHK(c, hipMalloc(&c->d_pack32, pb));
+        HIPCHK(c, hipMemcpy(c->d_pack32, pack.data(), pb, hipMemcpyHostToDevice));
+        c->mlp.pack32 = c->d_pack32;
+        c->mlp.pack32_bytes = (int)pb;
+        c->mlp.in0 = c->dims[0];
+        c->mlp.nh = nl - 2;
+    }
+    return upload_lowp(c);
+}
+
+int ensure_rays(nr_ctx *c, size_t n) {
+    if (n <= c->cap_rays) return NR_OK;
+    for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
+    dfree(c->d_SP); dfree(c->d_SD);
+    c->cap_rays = 0;
+    size_t b = std::max<size_t>(n, 64) * sizeof(float4);
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(c, hipMalloc(&c->d_P[i], b));
+        HIPCHK(c, hipMalloc(&c->d_D[i], b));
+    }
+    HIPCHK(c, hipMalloc(&c->d_SP, b));
+    HIPCHK(c, hipMalloc(&c->d_SD, b));
+    c->cap_rays = std::max<size_t>(n, 64);
+    return NR_OK;
+}
+
+int ensure_ctr(nr_ctx *c, size_t n) {
+    if (n <= c->cap_ctr) return NR_OK;
+    dfree(c->d_ctr);
+    if (c->h_ctr) { (void)hipHostFree(c->h_ctr); c->h_ctr = nullptr; }
+    c->cap_ctr = 0;
+    HIPCHK(c, hipMalloc(&c->d_ctr, n * 4));
+    HIPCHK(c, hipHostMalloc(&c->h_ctr, n * 4, hipHostMallocDefault));
+    c->cap_ctr = n;
+    return NR_OK;
+}
+
+template <class T>
+int ensure_buf(nr_ctx *c, T *&p, size_t &cap, size_t n) {
+    if (n <= cap) return NR_OK;
+    dfree(p);
+    cap = 0;
+    HIPCHK(c, hipMalloc(&p, std::max<size_t>(n, 64) * sizeof(T)));
+    cap = std::max<size_t>(n, 64);
+    return NR_OK;
+}
+
+// event pair for one launch when profiling; returns indices into ev_pool
+int prof_begin(nr_ctx *c, int kind, hipStream_t s) {
+    if (!c->profiling) return 0;
+    size_t need = c->recs.size() * 2 + 2;
+    while (c->ev_pool.size() < need) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreate(&e));
+        c->ev_pool.push_back(e);
+    }
+    int e0 = (int)c->recs.size() * 2;
+    c->recs.push_back({kind, e0, e0 + 1});
+    HIPCHK(c, hipEventRecord(c->ev_pool[e0], s));
+    return NR_OK;
+}
+int prof_end(nr_ctx *c, hipStream_t s) {
+    if (!c->profiling) return NR_OK;
+    HIPCHK(c, hipEventRecord(c->ev_pool[c->recs.back().e1], s));
+    return NR_OK;
+}
+
+int num_cus(int dev) {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    return cus;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nr_abi_version(void) { return NR_ABI_VERSION; }
+
+const char *nr_last_error(const nr_ctx *ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int nr_create(int device, nr_ctx **out) {
+    if (!out) return set_err(nullptr, NR_E_INVALID, "nr_create: out is NULL");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) return set_err(nullptr, NR_E_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= ndev) return set_err(nullptr, NR_E_INVALID, "device %d out of range (%d devices)", device, ndev);
+    nr_ctx *c = new (std::nothrow) nr_ctx();
+    if (!c) return set_err(nullptr, NR_E_NOMEM, "out of host memory");
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        delete c;
+        return set_err(nullptr, NR_E_HIP, "stream/event creation failed");
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return NR_OK;
+}
+
+int nr_destroy(nr_ctx *c) {
+    if (!c) return NR_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_network(c);
+    for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_io); dfree(c->d_matcap);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return NR_OK;
+}
+
+int nr_set_stream(nr_ctx *c, void *s) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    c->stream = s ? (hipStream_t)s : c->own_stream;
+    return NR_OK;
+}
+
+int nr_synchronize(nr_ctx *c) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return NR_OK;
+}
+
+int nr_load_h5(nr_ctx *c, const char *path) {
+    if (!c || !path) return set_err(c, NR_E_INVALID, "nr_load_h5: NULL argument");
+    std::vector<int> dims;
+    std::vector<std::vector<float>> K, B;
+    std::string err;
+    int rc = h5_read_keras(path, dims, K, B, err);
+    if (rc != NR_OK) return set_err(c, rc, "Failed to initialize model (%s): %s", path, err.c_str());
+    return set_network(c, std::move(dims), std::move(K), std::move(B));
+}
+
+int nr_load_mlp(nr_ctx *c, int nlayers, const int *dims, const float *const *kernels, const float *const *biases) {
+    if (!c || nlayers < 1 || !dims || !kernels || !biases) return set_err(c, NR_E_INVALID, "nr_load_mlp: bad arguments");
+    std::vector<int> d(dims, dims + nlayers + 1);
+    for (int v : d)
+        if (v < 1 || v > 4096) return set_err(c, NR_E_INVALID, "nr_load_mlp: layer size %d out of range", v);
+    std::vector<std::vector<float>> K(nlayers), B(nlayers);
+    for (int l = 0; l < nlayers; ++l) {
+        if (!kernels[l] || !biases[l]) return set_err(c, NR_E_INVALID, "nr_load_mlp: NULL layer %d", l);
+        K[l].assign(kernels[l], kernels[l] + (size_t)d[l] * d[l + 1]);
+        B[l].assign(biases[l], biases[l] + d[l + 1]);
+    }
+    return set_network(c, std::move(d), std::move(K), std::move(B));
+}
+
+int nr_mlp_info(const nr_ctx *c, int *nlayers, int *dims, int *nw, int *nb) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    int nl = c->dims.empty() ? 0 : (int)c->dims.size() - 1;
+    if (nlayers) *nlayers = nl;
+    int w = 0, b = 0;
+    for (int l = 0; l < nl; ++l) {
+        if (dims) dims[l] = c->dims[l];
+        w += c->dims[l] * c->dims[l + 1];
+        b += c->dims[l + 1];
+    }
+    if (dims && nl) dims[nl] = c->dims[nl];
+    if (nw) *nw = w;
+    if (nb) *nb = b;
+    return NR_OK;
+}
+
+int nr_set_precision(nr_ctx *c, int precision) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    if (precision < NR_PRECISION_FP32 || precision > NR_PRECISION_FP16)
+        return set_err(c, NR_E_INVALID, "unknown precision %d", precision);
+    c->precision = precision;
+    HIPCHK(c, hipSetDevice(c->device));
+    return upload_lowp(c);
+}
+
+int nr_set_view(nr_ctx *c, const float inv_view[12], const float normal[16], int frame) {
+    if (!c || !inv_view || !normal) return set_err(c, NR_E_INVALID, "nr_set_view: NULL argument");
+    memcpy(c->inv_view, inv_view, sizeof c->inv_view);
+    memcpy(c->normal, normal, sizeof c->normal);
+    c->frame = frame;
+    return NR_OK;
+}
+
+int nr_set_static(nr_ctx *c, int color_type, int num_inputs) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    if (color_type != NR_COLOR_FACING && color_type != NR_COLOR_MATCAP)
+        return set_err(c, NR_E_INVALID, "unknown color type %d", color_type);
+    if (num_inputs != 3 && num_inputs != 4) return set_err(c, NR_E_INVALID, "numInputs must be 3 or 4");
+    c->color_type = color_type;
+    c->num_inputs = num_inputs;
+    return NR_OK;
+}
+
+int nr_set_scene(nr_ctx *c, int scene) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    if (scene != NR_SCENE_V1 && scene != NR_SCENE_TANH) return set_err(c, NR_E_INVALID, "unknown scene %d", scene);
+    c->scene = scene;
+    return NR_OK;
+}
+
+int nr_set_matcap(nr_ctx *c, const uint32_t *rgba, int w, int h) {
+    if (!c || !rgba || w < 1 || h < 1) return set_err(c, NR_E_INVALID, "nr_set_matcap: bad arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    dfree(c->d_matcap);
+    HIPCHK(c, hipMalloc(&c->d_matcap, (size_t)w * h * 4));
+    HIPCHK(c, hipMemcpy(c->d_matcap, rgba, (size_t)w * h * 4, hipMemcpyHostToDevice));
+    c->mw = w; c->mh = h;
+    return NR_OK;
+}
+
+int nr_shard_rows(int H, int band, int nshards, int shard) {
+    if (H < 0 || band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return 0;
+    int full = H / band, rem = H % band;
+    int rows = (full / nshards) * band;
+    int extra = full % nshards;               // bands beyond the complete rounds
+    if (shard < extra) rows += band;
+    if (shard == extra && rem) rows += rem;   // the partial last band
+    return rows;
+}
+
+int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshards, int shard, int max_steps, int loc,
+                    nr_stats *stats) {
+    if (!c || !out) return set_err(c, NR_E_INVALID, "nr_render: NULL argument");
+    if (W < 1 || H < 1 || (long)W * H > (1l << 31)) return set_err(c, NR_E_INVALID, "nr_render: bad size %dx%d", W, H);
+    if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
+    if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
+    if (c->dims.empty()) return set_err(c, NR_E_STATE, "nr_render: no network loaded");
+    if (!c->fused)
+        return set_err(c, NR_E_FORMAT, "nr_render: network shape unsupported by the fused march kernel "
+                                       "(needs [3|4, 32, ..., 32, 1])");
+    if (c->dims[0] != c->num_inputs)
+        return set_err(c, NR_E_STATE, "nr_render: network takes %d inputs but numInputs = %d", c->dims[0], c->num_inputs);
+    if (c->color_type == NR_COLOR_MATCAP && !c->d_matcap) return set_err(c, NR_E_STATE, "nr_render: matcap colouring without a matcap");
+    HIPCHK(c, hipSetDevice(c->device));
+    int rows = nr_shard_rows(H, band, nshards, shard);
+    size_t npix = (size_t)W * rows;
+    nr_stats st{};
+    if (npix == 0) { if (stats) *stats = st; return NR_OK; }
+    int rc;
+    if ((rc = ensure_rays(c, npix)) != NR_OK) return rc;
+    if ((rc = ensure_ctr(c, (size_t)2 * max_steps + 8)) != NR_OK) return rc;
+    uint32_t *dout = out;
+    if (loc != NR_DEVICE) {
+        if ((rc = ensure_buf(c, c->d_out, c->cap_out, npix)) != NR_OK) return rc;
+        dout = c->d_out;
+    }
+    RenderArgs A{};
+    A.out = dout; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
+    A.max_steps = max_steps; A.scene = c->scene; A.frame = c->frame; A.color_type = c->color_type;
+    A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    memcpy(A.inv_view, c->inv_view, sizeof A.inv_view);
+    memcpy(A.normal, c->normal, sizeof A.normal);
+    // counters: [0, max_steps] live counts, [max_steps+1] shade count, [max_steps+2 ...] shade_it
+    uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + max_steps + 1, *shade_it = c->d_ctr + max_steps + 2;
+    size_t nctr = (size_t)2 * max_steps + 2;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, nctr * 4, s));
+    QueueArgs Q{};
+    Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
+    Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
+    int rc2;
+    if ((rc2 = prof_begin(c, 0, s)) != NR_OK) return rc2;
+    HIPCHK(c, launch_init(A, Q, s));
+    if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+    int launches = 2;
+    int cus = num_cus(c->device);
+    int march_grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * 4);
+    if (march_grid < 1) march_grid = 1;
+    for (int it = 0; it < max_steps; ++it) {
+        Q.cnt_in = cnt + it; Q.cnt_out = cnt + it + 1;
+        Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
+        Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
+        if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
+        HIPCHK(c, launch_march(A, c->mlp, Q, c->precision, it, march_grid, s));
+        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        ++launches;
+        if (c->check_every > 0 && (it + 1) % c->check_every == 0 && it + 1 < max_steps) {
+            HIPCHK(c, hipMemcpyAsync(c->h_ctr, cnt + it + 1, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            if (c->h_ctr[0] == 0) break;
+        }
+    }
+    int shade_grid = (int)std::min<size_t>((npix + 1023) / 1024, (size_t)cus * 4);
+    if (shade_grid < 1) shade_grid = 1;
+    if ((rc2 = prof_begin(c, 2, s)) != NR_OK) return rc2;
+    HIPCHK(c, launch_shade(A, c->mlp, Q, shade_grid, s));
+    if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+    if (c->profiling) c->prof_renders++;
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
+    if (stats) {
+        HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_ctr, nctr * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        uint64_t steps = 0;
+        int iters = 0;
+        for (int it = 0; it < max_steps; ++it) {
+            steps += c->h_ctr[it];
+            if (c->h_ctr[it]) iters = std::max(iters, it + 1);
+            if (c->h_ctr[max_steps + 2 + it]) iters = std::max(iters, std::min(it + 2, max_steps));
+        }
+        st.ray_steps = steps;
+        st.rays_hit = c->h_ctr[0];
+        st.rays_shaded = c->h_ctr[max_steps + 1];
+        st.shade_evals = 4ull * st.rays_shaded;
+        st.iterations = iters;
+        st.launches = launches;
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        st.ms_total = ms;
+        *stats = st;
+    } else if (loc != NR_DEVICE) {
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    return NR_OK;
+}
+
+int nr_render(nr_ctx *c, uint32_t *out, int W, int H, int max_steps, int loc, nr_stats *stats) {
+    return nr_render_shard(c, out, W, H, H > 0 ? H : 1, 1, 0, max_steps, loc, stats);
+}
+
+int nr_assemble_shards(nr_ctx *c, const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band,
+                       int nshards, int loc) {
+    if (!src || !dst || W < 1 || H < 1 || band < 1 || nshards < 1) return set_err(c, NR_E_INVALID, "nr_assemble_shards: bad arguments");
+    if (loc == NR_DEVICE) {
+        if (!c) return set_err(nullptr, NR_E_INVALID, "device assembly needs a context");
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, launch_assemble(src, stride, dst, W, H, band, nshards, c->stream));
+        return NR_OK;
+    }
+    for (int y = 0; y < H; ++y) {
+        int b = y / band, s = b % nshards, lr = (b / nshards) * band + y % band;
+        memcpy(dst + (size_t)y * W, src + (size_t)s * stride + (size_t)lr * W, (size_t)W * 4);
+    }
+    return NR_OK;
+}
+
+int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
+    if (!c || (n > 0 && (!X || !Y)) || n < 0) return set_err(c, NR_E_INVALID, "nr_mlp_forward: bad arguments");
+    if (c->dims.empty()) return set_err(c, NR_E_STATE, "nr_mlp_forward: no network loaded");
+    if (n == 0) return NR_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int nl = (int)c->dims.size() - 1, in0 = c->dims[0], outn = c->dims[nl];
+    hipStream_t s = c->stream;
+    const float *dX = X;
+    float *dY = Y;
+    int rc;
+    int maxw = *std::max_element(c->dims.begin(), c->dims.end());
+    size_t need = (loc == NR_DEVICE ? 0 : (size_t)n * (in0 + outn)) + (c->fused ? 0 : (size_t)2 * n * maxw);
+    if ((rc = ensure_buf(c, c->d_io, c->cap_io, need)) != NR_OK) return rc;
+    float *scratch = c->d_io;
+    if (loc != NR_DEVICE) {
+        float *hx = scratch; scratch += (size_t)n * in0;
+        dY = scratch; scratch += (size_t)n * outn;
+        HIPCHK(c, hipMemcpyAsync(hx, X, (size_t)n * in0 * 4, hipMemcpyHostToDevice, s));
+        dX = hx;
+    }
+    if (c->fused) {
+        int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * 4);
+        HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
+    } else {
+        const float *a = dX;
+        float *bufs[2] = {scratch, scratch + (size_t)n * maxw};
+        for (int l = 0; l < nl; ++l) {
+            float *z = (l == nl - 1) ? dY : bufs[l & 1];
+            HIPCHK(c, launch_dense(c->d_W[l], c->d_b[l], a, z, n, c->dims[l], c->dims[l + 1], l != nl - 1, s));
+            a = z;
+        }
+    }
+    if (loc != NR_DEVICE) {
+        HIPCHK(c, hipMemcpyAsync(Y, dY, (size_t)n * outn * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    return NR_OK;
+}
+
+int nr_layer_forward(nr_ctx *c, int layer, const float *A, float *Z, long n, int loc) {
+    if (!c || n < 0 || (n > 0 && (!A || !Z))) return set_err(c, NR_E_INVALID, "nr_layer_forward: bad arguments");
+    int nl = c->dims.empty() ? 0 : (int)c->dims.size() - 1;
+    if (layer < 0 || layer >= nl) return set_err(c, NR_E_INVALID, "nr_layer_forward: layer %d out of range", layer);
+    if (n == 0) return NR_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    int in = c->dims[layer], out = c->dims[layer + 1];
+    hipStream_t s = c->stream;
+    const float *dA = A;
+    float *dZ = Z;
+    if (loc != NR_DEVICE) {
+        int rc = ensure_buf(c, c->d_io, c->cap_io, (size_t)n * (in + out));
+        if (rc != NR_OK) return rc;
+        float *ha = c->d_io;
+        dZ = c->d_io + (size_t)n * in;
+        HIPCHK(c, hipMemcpyAsync(ha, A, (size_t)n * in * 4, hipMemcpyHostToDevice, s));
+        dA = ha;
+    }
+    HIPCHK(c, launch_dense(c->d_W[layer], c->d_b[layer], dA, dZ, n, in, out, layer != nl - 1, s));
+    if (loc != NR_DEVICE) {
+        HIPCHK(c, hipMemcpyAsync(Z, dZ, (size_t)n * out * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    return NR_OK;
+}
+
+int nr_set_profiling(nr_ctx *c, int on) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    c->profiling = on != 0;
+    return NR_OK;
+}
+
+int nr_prof_collect(nr_ctx *c, nr_kernel_prof *out) {
+    if (!c || !out) return set_err(c, NR_E_INVALID, "nr_prof_collect: NULL argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    nr_kernel_prof p{};
+    for (auto &r : c->recs) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev_pool[r.e0], c->ev_pool[r.e1]));
+        if (r.kind == 0) { p.init_ms += ms; p.init_launches++; }
+        else if (r.kind == 1) { p.march_ms += ms; p.march_launches++; }
+        else { p.shade_ms += ms; p.shade_launches++; }
+    }
+    p.renders = c->prof_renders;
+    c->recs.clear();
+    c->prof_renders = 0;
+    *out = p;
+    return NR_OK;
+}
+
+int nr_set_poll_interval(nr_ctx *c, int every) {
+    if (!c || every < 0) return set_err(c, NR_E_INVALID, "nr_set_poll_interval: bad arguments");
+    c->check_every = every;
+    return NR_OK;
+}
+
+int nr_camera(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {
+    if (!inv_view || !normal) return set_err(nullptr, NR_E_INVALID, "nr_camera: NULL output");
+    camera_matrices(rx, ry, zoom, tx, ty, inv_view, normal);
+    return NR_OK;
+}
+
+int nr_h5_read_keras(const char *path, int max_layers, int *nlayers, int *dims, float *params, size_t cap) {
+    if (!path || !nlayers) return set_err(nullptr, NR_E_INVALID, "nr_h5_read_keras: NULL argument");
+    std::vector<int> d;
+    std::vector<std::vector<float>> K, B;
+    std::string err;
+    int rc = h5_read_keras(path, d, K, B, err);
+    if (rc != NR_OK) return set_err(nullptr, rc, "%s", err.c_str());
+    int nl = (int)d.size() - 1;
+    *nlayers = nl;
+    if (dims) {
+        if (max_layers < nl) return set_err(nullptr, NR_E_INVALID, "nr_h5_read_keras: %d layers > max_layers", nl);
+        for (int i = 0; i <= nl; ++i) dims[i] = d[i];
+    }
+    if (params) {
+        size_t need = 0;
+        for (int l = 0; l < nl; ++l) need += K[l].size() + B[l].size();
+        if (cap < need) return set_err(nullptr, NR_E_INVALID, "nr_h5_read_keras: params buffer too small (%zu < %zu)", cap, need);
+        float *p = params;
+        for (int l = 0; l < nl; ++l) {
+            memcpy(p, K[l].data(), K[l].size() * 4); p += K[l].size();
+            memcpy(p, B[l].data(), B[l].size() * 4); p += B[l].size();
+        }
+    }
+    return NR_OK;
+}
+
+int nr_png_load(const char *path, uint32_t **rgba, int *w, int *h) {
+    if (!path || !rgba || !w || !h) return set_err(nullptr, NR_E_INVALID, "nr_png_load: NULL argument");
+    std::vector<uint32_t> px;
+    std::string err;
+    int rc = png_decode(path, px, *w, *h, err);
+    if (rc != NR_OK) return set_err(nullptr, rc, "Error reading png: %s", err.c_str());
+    *rgba = (uint32_t *)malloc(px.size() * 4);
+    if (!*rgba) return set_err(nullptr, NR_E_NOMEM, "out of memory");
+    memcpy(*rgba, px.data(), px.size() * 4);
+    return NR_OK;
+}
+
+int nr_png_save(const char *path, const uint32_t *rgba, int w, int h, int flip) {
+    if (!path || !rgba) return set_err(nullptr, NR_E_INVALID, "nr_png_save: NULL argument");
+    std::string err;
+    int rc = png_encode(path, rgba, w, h, flip, err);
+    if (rc != NR_OK) return set_err(nullptr, rc, "[ERROR] Unable to save png: %s", err.c_str());
+    return NR_OK;
+}
+
+int nr_ppm_save(const char *path, const uint32_t *rgba, int w, int h) {
+    if (!path || !rgba || w < 1 || h < 1) return set_err(nullptr, NR_E_INVALID, "nr_ppm_save: bad arguments");
+    std::string err;
+    int rc = ppm_encode(path, rgba, w, h, err);
+    if (rc != NR_OK) return set_err(nullptr, rc, "%s", err.c_str());
+    return NR_OK;
+}
+
+void nr_free(void *p) { free(p); }
+
+}  // extern "C"

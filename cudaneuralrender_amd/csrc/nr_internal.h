@@ -1,0 +1,58 @@
+// nr_internal.h -- declarations shared by the host side of libnr.so.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/neural_render.h"
+
+#if defined(__HIPCC__)
+#define NR_HD __host__ __device__
+#else
+#define NR_HD
+#endif
+
+namespace nr {
+
+// ---- host-side file formats (h5_keras.cpp, png_codec.cpp) ----
+int h5_read_keras(const char *path, std::vector<int> &dims, std::vector<std::vector<float>> &kernels,
+                  std::vector<std::vector<float>> &biases, std::string &err);
+int png_decode(const char *path, std::vector<uint32_t> &rgba, int &w, int &h, std::string &err);
+int png_encode(const char *path, const uint32_t *rgba, int w, int h, int flip, std::string &err);
+int ppm_encode(const char *path, const uint32_t *rgba, int w, int h, std::string &err);
+
+// ---- packed network layouts (nr_pack.cpp) ----
+// fp32 fused-path layout, in floats (see DESIGN.md "MLP on MFMA"):
+//   [0,128)    layer-0 weights  [half 2][reg 16][4]   (k = x, y, z, frame)
+//   [128,160)  layer-0 bias     [half 2][reg 16]
+//   per hidden layer j (0..nh-1), base 160 + j*1056:
+//              A operand        [group 4][lane 64][4] (MFMA step s = 4*group + e)
+//              bias             [half 2][reg 16]
+//   final:     weights [half 2][reg 16], bias [1] (+3 pad)
+constexpr int PK_L0W = 0;
+constexpr int PK_L0B = 128;
+constexpr int PK_HID = 160;
+constexpr int PK_HID_STRIDE = 1024 + 32;
+constexpr int MAX_HIDDEN = 16;
+NR_HD constexpr inline int pk_final(int nh) { return PK_HID + nh * PK_HID_STRIDE; }
+NR_HD constexpr inline int pk_floats(int nh) { return pk_final(nh) + 36; }
+
+// Low-precision (bf16/fp16) hidden-layer layout, in 16-bit elements per layer:
+//   A operand [kstep 2][lane 64][8]; followed (in a separate float array) by the
+//   bias [half 2][reg 16] in f32.  Layer 0 / final layer reuse the fp32 pack.
+constexpr int LP_A_ELEMS = 2 * 64 * 8;
+
+bool fused_shape_ok(const std::vector<int> &dims);
+// Keras kernels (in x out, row-major) -> packs.  Returns false if shape unsupported.
+bool pack_fp32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+               const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
+bool pack_lowp(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+               const std::vector<std::vector<float>> &biases, int precision,
+               std::vector<uint16_t> &a_ops, std::vector<float> &bias);
+
+// ---- camera (nr_camera.cpp) ----
+void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]);
+
+}  // namespace nr

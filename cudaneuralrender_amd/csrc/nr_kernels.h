@@ -1,0 +1,51 @@
+// nr_kernels.h -- kernel argument blocks and launchers (nr_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nr {
+
+// Network packs resident in device memory, staged into LDS by every block.
+struct MlpArgs {
+    const float *pack32;    // fp32 pack (nr_internal.h PK_*)
+    const uint16_t *lp;     // bf16/fp16 A operands (precision != fp32)
+    const float *lpf;       // float side of the low-precision pack
+    int pack32_bytes, lp_bytes, lpf_bytes;
+    int in0, nh;
+};
+
+// Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
+// passed by value so contexts are independent).
+struct RenderArgs {
+    uint32_t *out;          // this shard's rows, W per row
+    int W, H, rows, band, nshards, shard;
+    int max_steps, scene, frame, color_type;
+    const uint32_t *matcap;
+    int mw, mh;
+    float inv_view[12];
+    float normal[16];
+};
+
+// Ray queues: live rays {p.xyz, tfar} + {d.xyz, pixel}; converged rays {p.xyz, -} + {d.xyz, pixel}.
+struct QueueArgs {
+    const uint32_t *cnt_in;
+    uint32_t *cnt_out;
+    const float4 *p_in, *d_in;
+    float4 *p_out, *d_out;
+    uint32_t *shade_cnt;
+    float4 *shade_p, *shade_d;
+    uint32_t *shade_it;     // per-iteration count of waves that enqueued converged rays
+};
+
+int smem_bytes(const MlpArgs &M, int prec);
+hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
+hipError_t launch_dense(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
+                        hipStream_t st);
+hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st);
+hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int prec, int it, int grid,
+                        hipStream_t st);
+hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
+hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
+                           hipStream_t st);
+
+}  // namespace nr

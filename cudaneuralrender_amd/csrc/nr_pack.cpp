@@ -1,0 +1,163 @@
+// nr_pack.cpp -- host-side weight packing for the fused MFMA MLP, and the camera.
+//
+// Input: Keras Dense kernels (in x out, row-major) as HighFive hands them to the
+// DenseLayer constructor (reference src/layers/denseLayer.cu:180-227, which
+// transposes them to out-major W[out][in]).  Output: register-layout-ready packs
+// for the kernels in nr_kernels.hip (layout documented in nr_internal.h and
+// DESIGN.md "MLP on MFMA").
+#include "nr_internal.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace nr {
+
+bool fused_shape_ok(const std::vector<int> &dims) {
+    int nl = (int)dims.size() - 1;
+    if (nl < 2 || nl - 2 > MAX_HIDDEN) return false;
+    if (dims[0] != 3 && dims[0] != 4) return false;
+    for (int l = 1; l < nl; ++l) if (dims[l] != 32) return false;
+    return dims[nl] == 1;
+}
+
+namespace {
+// physical accumulator row of (lane half h, register r) for a 32x32 MFMA tile
+inline int acc_row(int h, int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// hidden unit held by (half h, register r) in the fp32 path: consumer = next MFMA
+// layer -> interleaved (2r + h) so that the f32 MFMA k-order is ascending; consumer
+// = final VALU layer -> halves (16h + r) so one cross-lane hand-off suffices.
+inline int unit_f32(int h, int r, bool final_consumer) { return final_consumer ? 16 * h + r : 2 * r + h; }
+
+uint16_t f2bf16(float x) {
+    uint32_t u; memcpy(&u, &x, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+uint16_t f2fp16(float x) {
+    uint32_t u; memcpy(&u, &x, 4);
+    uint32_t sign = (u >> 16) & 0x8000u;
+    float ax = std::fabs(x);
+    if (std::isnan(x)) return (uint16_t)(sign | 0x7e00u);
+    if (ax >= 65520.0f) return (uint16_t)(sign | 0x7c00u);
+    if (ax < 6.103515625e-05f) {                       // subnormal half
+        float q = std::nearbyint(ax / 5.9604644775390625e-08f);   // RNE (default rounding mode)
+        return (uint16_t)(sign | (uint32_t)q);
+    }
+    int e; float m = std::frexp(ax, &e);                // ax = m 2^e, m in [0.5,1)
+    float mant = std::nearbyint((m * 2.0f - 1.0f) * 1024.0f);
+    int exp = e - 1 + 15;
+    if (mant >= 1024.0f) { mant = 0; exp += 1; }
+    if (exp >= 31) return (uint16_t)(sign | 0x7c00u);
+    return (uint16_t)(sign | (uint32_t)exp << 10 | (uint32_t)mant);
+}
+}  // namespace
+
+bool pack_fp32(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+               const std::vector<std::vector<float>> &B, std::vector<float> &pack) {
+    if (!fused_shape_ok(dims)) return false;
+    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    pack.assign(pk_floats(nh), 0.0f);
+    // layer 0 (VALU): K[0] is (in0 x 32)
+    for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) {
+            int u = unit_f32(h, r, nh == 0);
+            for (int k = 0; k < 4; ++k)
+                pack[PK_L0W + (h * 16 + r) * 4 + k] = (k < in0) ? K[0][(size_t)k * 32 + u] : 0.0f;
+            pack[PK_L0B + h * 16 + r] = B[0][u];
+        }
+    // hidden 32x32 layers on v_mfma_f32_32x32x2_f32
+    for (int j = 0; j < nh; ++j) {
+        const std::vector<float> &Kj = K[j + 1];
+        bool fin = (j == nh - 1);
+        int base = PK_HID + j * PK_HID_STRIDE;
+        for (int s = 0; s < 16; ++s)
+            for (int lane = 0; lane < 64; ++lane) {
+                int i = lane & 31, kk = lane >> 5;
+                int hi = (i >> 2) & 1, si = (i & 3) + 4 * (i >> 3);
+                int uout = fin ? 16 * hi + si : 2 * si + hi;
+                int uin = 2 * s + kk;
+                pack[base + ((s >> 2) * 64 + lane) * 4 + (s & 3)] = Kj[(size_t)uin * 32 + uout];
+            }
+        for (int h = 0; h < 2; ++h)
+            for (int r = 0; r < 16; ++r) pack[base + 1024 + h * 16 + r] = B[j + 1][unit_f32(h, r, fin)];
+    }
+    // final 32 -> 1 (VALU): half h register r holds unit 16h + r (or 2r + h when nh == 0... see below)
+    int fo = pk_final(nh);
+    for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) pack[fo + h * 16 + r] = K[nl - 1][16 * h + r];
+    pack[fo + 32] = B[nl - 1][0];
+    return true;
+}
+
+bool pack_lowp(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+               const std::vector<std::vector<float>> &B, int precision, std::vector<uint16_t> &a_ops,
+               std::vector<float> &fl) {
+    if (!fused_shape_ok(dims)) return false;
+    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    auto cvt = [&](float v) { return precision == NR_PRECISION_BF16 ? f2bf16(v) : f2fp16(v); };
+    a_ops.assign((size_t)nh * LP_A_ELEMS, 0);
+    // float side: [L0W 128][L0B 32][hidden bias 32 x nh][final w 32][final b 1 + 3 pad]
+    fl.assign(160 + 32 * nh + 36, 0.0f);
+    for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) {
+            int u = acc_row(h, r);
+            for (int k = 0; k < 4; ++k) fl[(h * 16 + r) * 4 + k] = (k < in0) ? K[0][(size_t)k * 32 + u] : 0.0f;
+            fl[128 + h * 16 + r] = B[0][u];
+        }
+    for (int j = 0; j < nh; ++j) {
+        const std::vector<float> &Kj = K[j + 1];
+        for (int ks = 0; ks < 2; ++ks)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    int i = lane & 31, hh = lane >> 5;
+                    int uin = 16 * ks + 8 * (e >> 2) + 4 * hh + (e & 3);
+                    a_ops[(size_t)j * LP_A_ELEMS + (ks * 64 + lane) * 8 + e] = cvt(Kj[(size_t)uin * 32 + i]);
+                }
+        for (int h = 0; h < 2; ++h)
+            for (int r = 0; r < 16; ++r) fl[160 + 32 * j + h * 16 + r] = B[j + 1][acc_row(h, r)];
+    }
+    int fo = 160 + 32 * nh;
+    for (int h = 0; h < 2; ++h)
+        for (int r = 0; r < 16; ++r) fl[fo + h * 16 + r] = K[nl - 1][acc_row(h, r)];
+    fl[fo + 32] = B[nl - 1][0];
+    return true;
+}
+
+// updateViewMatrices (reference src/main.cpp:207-222), evaluated in double and
+// rounded to float once (the reference uses Eigen float arithmetic).
+void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {
+    const double pi = 3.14159265358979323846;
+    double ax = -(double)rx * pi / 180.0, ay = -(double)ry * pi / 180.0;
+    double cx = std::cos(ax), sx = std::sin(ax), cy = std::cos(ay), sy = std::sin(ay);
+    double Rx[3][3] = {{1, 0, 0}, {0, cx, -sx}, {0, sx, cx}};
+    double Ry[3][3] = {{cy, 0, sy}, {0, 1, 0}, {-sy, 0, cy}};
+    double R[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            R[i][j] = 0;
+            for (int k = 0; k < 3; ++k) R[i][j] += Rx[i][k] * Ry[k][j];
+        }
+    // viewTranslation = (tx, ty, -zoom); modelView.translate(-viewTranslation)
+    double t[3] = {-(double)tx, -(double)ty, (double)zoom};
+    double T[3];
+    for (int i = 0; i < 3; ++i) T[i] = R[i][0] * t[0] + R[i][1] * t[1] + R[i][2] * t[2];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) inv_view[4 * i + j] = (float)R[i][j];
+        inv_view[4 * i + 3] = (float)T[i];
+    }
+    // inverse of [R | T; 0 1] = [R^T | -R^T T; 0 1]
+    for (int i = 0; i < 3; ++i) {
+        double acc = 0;
+        for (int j = 0; j < 3; ++j) {
+            normal[4 * i + j] = (float)R[j][i];
+            acc += R[j][i] * T[j];
+        }
+        normal[4 * i + 3] = (float)(-acc);
+    }
+    normal[12] = normal[13] = normal[14] = 0.0f;
+    normal[15] = 1.0f;
+}
+
+}  // namespace nr

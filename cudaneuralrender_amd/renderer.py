@@ -1,0 +1,245 @@
+"""Python host side of the renderer: a thin object wrapper over the C ABI.
+
+Mirrors the reference's host flow (src/main.cpp:636-678 -> generateSingleImage
+:404-468): load the network (NeuralNetwork::load), optionally a matcap
+(Image::loadPNG), copyStaticSettings, updateViewMatrices + copyViewMatrices, then
+render_kernel.  All compute runs in libnr.so on the GPU.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_HOST, NR_PRECISION, NR_SCENE,
+                   NRKernelProf, NRStats, check, lib)
+
+_FP = ctypes.POINTER(ctypes.c_float)
+
+
+def _fptr(a):
+    return a.ctypes.data_as(_FP)
+
+
+def camera(rx=0.0, ry=0.0, zoom=2.0, tx=0.0, ty=0.0):
+    """updateViewMatrices (main.cpp:207-222): returns (inv_view[12], normal[16]) float32.
+
+    ``zoom`` is the value of the reference's ``-z`` flag (default 2): the eye sits at
+    R * (tx, ty, zoom)... i.e. viewTranslation = (tx, ty, -zoom)."""
+    iv = np.zeros(12, np.float32)
+    nm = np.zeros(16, np.float32)
+    check(lib().nr_camera(rx, ry, zoom, tx, ty, _fptr(iv), _fptr(nm)))
+    return iv, nm
+
+
+def read_keras_h5(path):
+    """NeuralNetwork::load's reader (neuralNetwork.cpp:85-151) without a device:
+    returns (dims, [kernel (in, out)], [bias (out,)])."""
+    L = lib()
+    nl = ctypes.c_int(0)
+    check(L.nr_h5_read_keras(path.encode(), 0, ctypes.byref(nl), None, None, 0))
+    dims = (ctypes.c_int * (nl.value + 1))()
+    check(L.nr_h5_read_keras(path.encode(), nl.value, ctypes.byref(nl), dims, None, 0))
+    dims = list(dims)
+    total = sum(dims[i] * dims[i + 1] + dims[i + 1] for i in range(nl.value))
+    buf = np.zeros(total, np.float32)
+    check(L.nr_h5_read_keras(path.encode(), nl.value, ctypes.byref(nl), None, _fptr(buf), total))
+    kernels, biases, off = [], [], 0
+    for i in range(nl.value):
+        n = dims[i] * dims[i + 1]
+        kernels.append(buf[off:off + n].reshape(dims[i], dims[i + 1]).copy())
+        off += n
+        biases.append(buf[off:off + dims[i + 1]].copy())
+        off += dims[i + 1]
+    return dims, kernels, biases
+
+
+def load_png(path):
+    """Image::loadPNG (image.cu:36-65): (h, w) uint32 packed a<<24|b<<16|g<<8|r."""
+    L = lib()
+    p = ctypes.POINTER(ctypes.c_uint32)()
+    w, h = ctypes.c_int(0), ctypes.c_int(0)
+    check(L.nr_png_load(path.encode(), ctypes.byref(p), ctypes.byref(w), ctypes.byref(h)))
+    try:
+        arr = np.ctypeslib.as_array(p, shape=(h.value * w.value,)).copy().reshape(h.value, w.value)
+    finally:
+        L.nr_free(ctypes.cast(p, ctypes.c_void_p))
+    return arr
+
+
+def save_png(path, img, flip=True):
+    """Image::savePNG (image.cu:67-110); flip=True is the reference's 180-degree rotation."""
+    img = np.ascontiguousarray(img, dtype=np.uint32)
+    check(lib().nr_png_save(path.encode(), img.ctypes.data, img.shape[1], img.shape[0], int(flip)))
+
+
+def save_ppm(path, img):
+    img = np.ascontiguousarray(img, dtype=np.uint32)
+    check(lib().nr_ppm_save(path.encode(), img.ctypes.data, img.shape[1], img.shape[0]))
+
+
+def shard_rows(H, band, nshards, shard):
+    return lib().nr_shard_rows(H, band, nshards, shard)
+
+
+def assemble_shards(shards, W, H, band, nshards):
+    """Host re-interleave of gathered shards (list or stacked array, each padded to a
+    common stride) into the full frame."""
+    stride = max(shard_rows(H, band, nshards, s) for s in range(nshards)) * W
+    buf = np.zeros((nshards, stride), np.uint32)
+    for s, sh in enumerate(shards):
+        a = np.asarray(sh, np.uint32).reshape(-1)
+        buf[s, :a.size] = a
+    out = np.zeros((H, W), np.uint32)
+    check(lib().nr_assemble_shards(None, buf.ctypes.data, stride, out.ctypes.data, W, H, band, nshards, NR_HOST))
+    return out
+
+
+class Renderer:
+    """One renderer context per GPU (nr_ctx)."""
+
+    def __init__(self, device=0):
+        self._L = lib()
+        self._ctx = ctypes.c_void_p()
+        check(self._L.nr_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+
+    # -- lifecycle
+    def close(self):
+        if self._ctx:
+            self._L.nr_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc):
+        return check(rc, self._ctx)
+
+    # -- network
+    def load_h5(self, path):
+        self._chk(self._L.nr_load_h5(self._ctx, path.encode()))
+        return self
+
+    def load_mlp(self, dims, kernels, biases):
+        nl = len(kernels)
+        d = (ctypes.c_int * (nl + 1))(*dims)
+        ks = [np.ascontiguousarray(k, np.float32) for k in kernels]
+        bs = [np.ascontiguousarray(b, np.float32) for b in biases]
+        kp = (_FP * nl)(*[_fptr(k) for k in ks])
+        bp = (_FP * nl)(*[_fptr(b) for b in bs])
+        self._chk(self._L.nr_load_mlp(self._ctx, nl, d, kp, bp))
+        return self
+
+    def mlp_info(self):
+        nl, nw, nb = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        dims = (ctypes.c_int * 64)()
+        self._chk(self._L.nr_mlp_info(self._ctx, ctypes.byref(nl), dims, ctypes.byref(nw), ctypes.byref(nb)))
+        return {"nlayers": nl.value, "dims": list(dims[:nl.value + 1]), "weights": nw.value, "biases": nb.value}
+
+    def set_precision(self, precision):
+        self._chk(self._L.nr_set_precision(self._ctx, NR_PRECISION[precision] if isinstance(precision, str) else precision))
+        return self
+
+    # -- settings
+    def set_view(self, inv_view, normal, frame=0):
+        iv = np.ascontiguousarray(inv_view, np.float32).reshape(12)
+        nm = np.ascontiguousarray(normal, np.float32).reshape(16)
+        self._chk(self._L.nr_set_view(self._ctx, _fptr(iv), _fptr(nm), int(frame)))
+        return self
+
+    def set_camera(self, rx=0.0, ry=0.0, zoom=2.0, frame=0):
+        iv, nm = camera(rx, ry, zoom)
+        return self.set_view(iv, nm, frame)
+
+    def set_static(self, color_type=NR_COLOR_FACING, num_inputs=3):
+        self._chk(self._L.nr_set_static(self._ctx, int(color_type), int(num_inputs)))
+        return self
+
+    def set_scene(self, scene):
+        self._chk(self._L.nr_set_scene(self._ctx, NR_SCENE[scene] if isinstance(scene, str) else int(scene)))
+        return self
+
+    def set_matcap(self, rgba):
+        m = np.ascontiguousarray(rgba, np.uint32)
+        self._chk(self._L.nr_set_matcap(self._ctx, m.ctypes.data, m.shape[1], m.shape[0]))
+        return self
+
+    def set_stream(self, stream_ptr):
+        self._chk(self._L.nr_set_stream(self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def set_profiling(self, on=True):
+        self._chk(self._L.nr_set_profiling(self._ctx, int(on)))
+
+    def prof_collect(self):
+        p = NRKernelProf()
+        self._chk(self._L.nr_prof_collect(self._ctx, ctypes.byref(p)))
+        return p.as_dict()
+
+    def set_poll_interval(self, every):
+        self._chk(self._L.nr_set_poll_interval(self._ctx, int(every)))
+
+    def synchronize(self):
+        self._chk(self._L.nr_synchronize(self._ctx))
+
+    # -- hot path
+    def render(self, W, H, max_steps=6000, with_stats=True):
+        out = np.zeros((H, W), np.uint32)
+        st = NRStats()
+        self._chk(self._L.nr_render(self._ctx, out.ctypes.data, W, H, max_steps, NR_HOST,
+                                    ctypes.byref(st) if with_stats else None))
+        return (out, st.as_dict()) if with_stats else out
+
+    def render_device(self, out_ptr, W, H, max_steps=6000, with_stats=False):
+        """Render into a device buffer (e.g. a torch tensor's data_ptr())."""
+        st = NRStats()
+        self._chk(self._L.nr_render(self._ctx, ctypes.c_void_p(out_ptr), W, H, max_steps, NR_DEVICE,
+                                    ctypes.byref(st) if with_stats else None))
+        return st.as_dict() if with_stats else None
+
+    def render_shard(self, W, H, band, nshards, shard, max_steps=6000, with_stats=True):
+        rows = shard_rows(H, band, nshards, shard)
+        out = np.zeros((rows, W), np.uint32)
+        st = NRStats()
+        self._chk(self._L.nr_render_shard(self._ctx, out.ctypes.data, W, H, band, nshards, shard, max_steps,
+                                          NR_HOST, ctypes.byref(st) if with_stats else None))
+        return (out, st.as_dict()) if with_stats else out
+
+    def render_shard_device(self, out_ptr, W, H, band, nshards, shard, max_steps=6000, with_stats=False):
+        st = NRStats()
+        self._chk(self._L.nr_render_shard(self._ctx, ctypes.c_void_p(out_ptr), W, H, band, nshards, shard,
+                                          max_steps, NR_DEVICE, ctypes.byref(st) if with_stats else None))
+        return st.as_dict() if with_stats else None
+
+    def assemble_device(self, src_ptr, stride, dst_ptr, W, H, band, nshards):
+        self._chk(self._L.nr_assemble_shards(self._ctx, ctypes.c_void_p(src_ptr), stride, ctypes.c_void_p(dst_ptr),
+                                             W, H, band, nshards, NR_DEVICE))
+
+    def mlp_forward(self, X):
+        X = np.ascontiguousarray(X, np.float32)
+        info = self.mlp_info()
+        n = X.shape[0]
+        Y = np.zeros((n, info["dims"][-1]), np.float32)
+        self._chk(self._L.nr_mlp_forward(self._ctx, X.ctypes.data, Y.ctypes.data, n, NR_HOST))
+        return Y
+
+    def mlp_forward_device(self, x_ptr, y_ptr, n):
+        self._chk(self._L.nr_mlp_forward(self._ctx, ctypes.c_void_p(x_ptr), ctypes.c_void_p(y_ptr), n, NR_DEVICE))
+
+    def layer_forward(self, layer, A):
+        A = np.ascontiguousarray(A, np.float32)
+        info = self.mlp_info()
+        Z = np.zeros((A.shape[0], info["dims"][layer + 1]), np.float32)
+        self._chk(self._L.nr_layer_forward(self._ctx, layer, A.ctypes.data, Z.ctypes.data, A.shape[0], NR_HOST))
+        return Z
+
+
+__all__ = ["Renderer", "camera", "read_keras_h5", "load_png", "save_png", "save_ppm", "shard_rows",
+           "assemble_shards", "NR_COLOR_FACING", "NR_COLOR_MATCAP"]

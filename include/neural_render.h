@@ -1,0 +1,167 @@
+/*
+ * neural_render.h -- C ABI of libnr.so, the MI355X (gfx950) neural-SDF renderer.
+ *
+ * Drop-in boundary for the reference's hot path (daviesthomas/cudaNeuralRender @ v1):
+ * the sphere-trace loop of src/volumeRender_kernel.cu and the batched dense-layer
+ * forward of src/layers/denseLayer.cu + src/neuralNetwork.cpp.  Every entry point
+ * takes plain pointers and sizes; state lives in an opaque per-device context
+ * (the reference keeps it in non-reentrant globals, volumeRender_kernel.cu:31-35,
+ * :578-585).  Functions return NR_OK (0) or a negative NR_E* code; the message is
+ * available from nr_last_error().  Nothing in the library calls exit()/abort()
+ * (the reference exits inside checkCudaErrors, helper_cuda.h:576-591).
+ *
+ * Threading: one context per GPU; calls on one context are not thread-safe, calls
+ * on different contexts are.  Each context owns one HIP stream.
+ */
+#ifndef NEURAL_RENDER_H
+#define NEURAL_RENDER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NR_ABI_VERSION 1
+
+/* status codes */
+#define NR_OK 0
+#define NR_E_INVALID (-1)    /* bad argument */
+#define NR_E_HIP (-2)        /* HIP runtime error */
+#define NR_E_IO (-3)         /* file missing / unreadable */
+#define NR_E_FORMAT (-4)     /* unsupported HDF5 / PNG content */
+#define NR_E_STATE (-5)      /* call out of order (e.g. render before load) */
+#define NR_E_NOMEM (-6)
+
+/* MLP arithmetic for the 32x32 hidden layers */
+#define NR_PRECISION_FP32 0  /* bit-exact with the CPU oracle (f32 MFMA = fmaf chain) */
+#define NR_PRECISION_BF16 1  /* bf16 MFMA, f32 accumulate; normals evaluated in fp32 */
+#define NR_PRECISION_FP16 2  /* fp16 MFMA, f32 accumulate; normals evaluated in fp32 */
+
+/* scene composition, sceneSDF (volumeRender_kernel.cu:217-230) */
+#define NR_SCENE_V1 0        /* v1: manySphere(p, nSDF, true) -- 9-sphere smooth union (:222) */
+#define NR_SCENE_TANH 1      /* tanh(nSDF), the pure neural surface (:229) */
+
+/* colouring, c_coloringType (volumeRender_kernel.cu:33) */
+#define NR_COLOR_FACING 0    /* facingColor (:380-384) */
+#define NR_COLOR_MATCAP 1    /* matCapColor (:387-413) */
+
+/* buffer location flags */
+#define NR_HOST 0
+#define NR_DEVICE 1
+
+typedef struct nr_ctx nr_ctx;
+
+typedef struct nr_stats {
+    uint64_t ray_steps;      /* MLP evaluations of marching rays (one per live ray per iteration) */
+    uint64_t shade_evals;    /* MLP evaluations for tetrahedral normals (4 per coloured ray) */
+    uint64_t rays_hit;       /* rays that entered the bounding sphere */
+    uint64_t rays_shaded;    /* pixels coloured */
+    int32_t iterations;      /* march iterations that had live rays (reference host-loop count) */
+    int32_t launches;        /* kernel launches issued */
+    float ms_total;          /* device time of the render, HIP events */
+} nr_stats;
+
+/* ---- context ------------------------------------------------------------ */
+int nr_create(int device, nr_ctx **out);
+int nr_destroy(nr_ctx *ctx);
+/* Last error of this context (ctx may be NULL: last error of the calling thread). */
+const char *nr_last_error(const nr_ctx *ctx);
+int nr_abi_version(void);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
+int nr_set_stream(nr_ctx *ctx, void *hip_stream);
+int nr_synchronize(nr_ctx *ctx);
+
+/* ---- network (NeuralNetwork::load / DenseLayer ctor) ---------------------- */
+/* Replaces NeuralNetwork::load(fp) (neuralNetwork.cpp:85-151): root groups in HDF5
+ * name order, each holding one subgroup with "bias:0" (1-D) and "kernel:0" (2-D,
+ * Keras (in, out)); last layer linear, others ReLU. */
+int nr_load_h5(nr_ctx *ctx, const char *path);
+/* Replaces DenseLayer(name, weights, biases, act) x nlayers (denseLayer.cu:180-227).
+ * dims[nlayers+1]; kernels[l] is the Keras (in=dims[l], out=dims[l+1]) row-major
+ * matrix, biases[l] has dims[l+1] floats.  ReLU on all layers but the last. */
+int nr_load_mlp(nr_ctx *ctx, int nlayers, const int *dims,
+                const float *const *kernels, const float *const *biases);
+int nr_mlp_info(const nr_ctx *ctx, int *nlayers, int *dims /* >= nlayers+1 or NULL */,
+                int *num_weight_params, int *num_bias_params);
+int nr_set_precision(nr_ctx *ctx, int precision);
+
+/* ---- per-frame settings (copyViewMatrices / copyStaticSettings) ---------- */
+/* Replaces copyViewMatrices (volumeRender_kernel.cu:694-700): inv_view = rows 0..2
+ * of the model-view matrix (3x4 row-major, c_invViewMatrix), normal = its inverse
+ * (4x4 row-major, c_normalMatrix), frame = c_frameNumber. */
+int nr_set_view(nr_ctx *ctx, const float inv_view[12], const float normal[16], int frame);
+/* Replaces copyStaticSettings (volumeRender_kernel.cu:702-706). */
+int nr_set_static(nr_ctx *ctx, int color_type, int num_inputs);
+int nr_set_scene(nr_ctx *ctx, int scene);
+/* Replaces Image::loadPNG + the matcap argument of render_kernel (image.cu:36-65):
+ * w*h texels packed a<<24 | b<<16 | g<<8 | r, row 0 = first PNG row. */
+int nr_set_matcap(nr_ctx *ctx, const uint32_t *rgba, int w, int h);
+
+/* ---- the hot path --------------------------------------------------------- */
+/* Replaces render_kernel (volumeRender_kernel.cu:608-692): renders a W x H frame,
+ * at most max_steps march iterations (reference MAX_STEPS = 6000), into out
+ * (W*H packed RGBA, row y*W + x, unconverged / missed pixels 0).  out_loc is
+ * NR_HOST or NR_DEVICE.  stats may be NULL. */
+int nr_render(nr_ctx *ctx, uint32_t *out, int W, int H, int max_steps, int out_loc,
+              nr_stats *stats);
+/* Multi-GPU shard of a frame: rows are dealt in bands of band_rows, band b goes to
+ * shard b % nshards.  out receives this shard's rows only, in increasing y
+ * (nr_shard_rows() of them, each W wide).  Pixels are identical to the same rows
+ * of nr_render. */
+int nr_render_shard(nr_ctx *ctx, uint32_t *out, int W, int H, int band_rows,
+                    int nshards, int shard, int max_steps, int out_loc, nr_stats *stats);
+int nr_shard_rows(int H, int band_rows, int nshards, int shard);
+/* Re-interleave gathered shards (shard s's rows at src + s*stride_pixels) into a full
+ * frame.  Host or device buffers (loc applies to both). */
+int nr_assemble_shards(nr_ctx *ctx, const uint32_t *src, size_t stride_pixels,
+                       uint32_t *dst, int W, int H, int band_rows, int nshards, int loc);
+
+/* Replaces NeuralNetwork::forward(X) (neuralNetwork.cpp:54-63) on a batch:
+ * X [n][dims[0]] fp32, Y [n][dims[nlayers]] fp32.  loc = NR_HOST or NR_DEVICE. */
+int nr_mlp_forward(nr_ctx *ctx, const float *X, float *Y, long n, int loc);
+/* One DenseLayer::forward (denseLayer.cu:229-278) on device buffers: layer l of the
+ * loaded network applied to A [n][dims[l]] -> Z [n][dims[l+1]]. */
+int nr_layer_forward(nr_ctx *ctx, int layer, const float *A, float *Z, long n, int loc);
+
+/* ---- measurement ------------------------------------------------------------ */
+/* Per-launch HIP events around every kernel of nr_render* on the context's stream
+ * (the stream those kernels run on).  nr_prof_collect() waits for the stream, sums
+ * the recorded durations since the previous collect and resets them. */
+typedef struct nr_kernel_prof {
+    double march_ms;         /* sum over k_march launches */
+    double shade_ms;         /* sum over k_shade launches */
+    double init_ms;          /* sum over k_init launches */
+    uint64_t march_launches, shade_launches, init_launches;
+    uint64_t renders;        /* nr_render* calls covered */
+} nr_kernel_prof;
+int nr_set_profiling(nr_ctx *ctx, int on);
+int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
+/* Host polls the live-ray count every `every` iterations to stop early (0 = never). */
+int nr_set_poll_interval(nr_ctx *ctx, int every);
+
+/* ---- host helpers (the reference's main.cpp / image.cu side) -------------- */
+/* updateViewMatrices (main.cpp:207-222): M = Rx(-rx deg) * Ry(-ry deg), then
+ * translate(-(tx, ty, -zoom)); inv_view = rows 0..2 of M, normal = M^-1. */
+int nr_camera(float rx_deg, float ry_deg, float zoom, float tx, float ty,
+              float inv_view[12], float normal[16]);
+/* Minimal HDF5 (superblock v0, symbol-table groups, contiguous datasets) Keras
+ * reader.  Call with kernels/biases NULL to query sizes. */
+int nr_h5_read_keras(const char *path, int max_layers, int *nlayers, int *dims,
+                     float *params /* per layer: kernel (in x out) then bias, or NULL */,
+                     size_t params_cap);
+/* PNG decode to packed RGBA (image.cu:36-65 packing).  *rgba is malloc'ed; free
+ * with nr_free(). */
+int nr_png_load(const char *path, uint32_t **rgba, int *w, int *h);
+/* Image::savePNG (image.cu:67-110): flip=1 reproduces the reference's 180 deg
+ * rotation (quirk Q9). */
+int nr_png_save(const char *path, const uint32_t *rgba, int w, int h, int flip);
+/* sdkSavePPM4ub-style P6 (helper_image.h:310-328), buffer row 0 first. */
+int nr_ppm_save(const char *path, const uint32_t *rgba, int w, int h);
+void nr_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEURAL_RENDER_H */

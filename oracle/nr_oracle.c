@@ -1,0 +1,501 @@
+/*
+ * nr_oracle.c -- CPU ORACLE for the neural-SDF sphere-trace hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library.  The product path (libnr.so) never
+ * links, calls or falls back to it.
+ *
+ * What it restates (reference = daviesthomas/cudaNeuralRender @ v1):
+ *   - DenseLayer forward       src/layers/denseLayer.cu:126-176, 229-278
+ *       Z_b[m] = act( sum_k W[m][k] * A_b[k] + bias[m] ), W stored out-major with `in`
+ *       contiguous (denseLayer.cu:217-227).  The accumulation is defined as the
+ *       ascending-k fmaf chain starting from +0, then "+ bias" (CUTLASS SIMT
+ *       mainloop + LinearCombination epilogue with alpha = beta = 1).  act = ReLU for
+ *       every layer but the last, which is LINEAR although tagged Tanh
+ *       (neuralNetwork.cpp:136-139, denseLayer.cu:150-166; quirk Q8).
+ *   - NeuralNetwork::forward    src/neuralNetwork.cpp:54-63 (chain of layers)
+ *   - render_kernel host loop   src/volumeRender_kernel.cu:608-692 with
+ *       initMarcher :293-358, formatInferenceReqs :549-576 (exclusive scan +
+ *       createBatch :504-547), singleMarch :416-477, surfaceNormal :361-377,
+ *       matCapColor :387-413, facingColor :380-384, rgbaFloatToInt :266-274,
+ *       sceneSDF :217-230 (v1: manySphere :177-196 smooth union :145-149;
+ *       tanh variant :229), intersectSphere :200-215, float3 helpers
+ *       (helper_math.h dot/length/normalize :1248-1313).
+ *   The loop is restated in the reference's own shape (full-image masks, an
+ *   exclusive scan, a packed batch, one MLP call per iteration) so that it is
+ *   an independent formulation from the GPU's per-ray queues.
+ *
+ * Arithmetic contract (shared with the HIP kernels, DESIGN.md "numerics"):
+ *   compiled with -ffp-contract=off; every mixed float/double expression of the
+ *   CUDA source is evaluated with C++ promotion rules (double literals such as
+ *   0.5, 0.6, 2.0 promote); sqrtf / division correctly rounded;
+ *   normalize(v) = v * (1.0f / sqrtf(dot(v,v)))  (reference: rsqrtf, an
+ *   approximation nvcc does not pin down); float->int conversion of NaN is 0 and
+ *   saturates (CUDA cvt.rzi semantics, quirk Q7).
+ *
+ * Deviations from v1, each documented in DESIGN.md:
+ *   Q1  the reference's batchSize omits the last pixel's mask (:553-562) so that
+ *       pixel reads stale SDF values; here the last pixel is marched like every
+ *       other pixel.
+ *   tanh the reference calls CUDA tanhf; here tanh is nr_tanh_f below, built
+ *       only from IEEE basic double operations so that CPU and GPU agree bit for bit.
+ *   anim with numInputs == 4 the reference writes normal-estimation points with a
+ *       stride of 3 (:538-545), leaving 4-input batches partly uninitialised; here
+ *       every batch point is (x, y, z, frame).
+ *
+ * Parity pinning: the reference cannot be built here (nvcc, CUTLASS, HighFive,
+ * Eigen, GLUT absent).  The oracle is pinned by (1) the weights read by h5py
+ * (tests/golden/weights_h5py.npz), (2) an fp64 numpy MLP (tests/golden/mlp_kat.npz),
+ * (3) simpleInfer's batch self-consistency check (simpleInfer.cpp:112-147) and
+ * (4) the silhouettes of the reference's own renders neuralGeometries/<geometry>.h5.ppm
+ * (tests/golden/silhouettes.npz).  Pixel colours are NOT pinned by any reference
+ * artefact (the .ppm shading predates v1), so pixel parity is
+ * "partial": coverage pinned, shading restated.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define OR_MAX_LAYERS 32
+
+typedef struct { float x, y, z; } f3;
+
+static const float TET[12] = { 1, -1, -1,  -1, -1, 1,  -1, 1, -1,  1, 1, 1 }; /* :38-43 */
+static const float NORMAL_EPSILON = 0.00001;     /* :59 */
+static const float MARCHING_EPSILON = 0.000001;  /* :60 */
+static const unsigned COLOR_MASK_VAL = 4;        /* :58 */
+
+/* ---------------------------------------------------------------- MLP */
+
+typedef struct {
+    int nlayers;
+    const int *dims;          /* nlayers + 1 */
+    const float *W[OR_MAX_LAYERS];  /* out-major [out][in] */
+    const float *b[OR_MAX_LAYERS];
+    int maxw;
+} or_mlp;
+
+static int or_mlp_init(or_mlp *m, int nlayers, const int *dims, const float *params)
+{
+    if (nlayers < 1 || nlayers > OR_MAX_LAYERS) return -1;
+    m->nlayers = nlayers;
+    m->dims = dims;
+    m->maxw = 0;
+    const float *p = params;
+    for (int l = 0; l < nlayers; ++l) {
+        int in = dims[l], out = dims[l + 1];
+        if (in < 1 || out < 1) return -1;
+        m->W[l] = p; p += (size_t)in * out;
+        m->b[l] = p; p += out;
+        if (in > m->maxw) m->maxw = in;
+        if (out > m->maxw) m->maxw = out;
+    }
+    return 0;
+}
+
+/* precision: 0 = fp32 (the parity contract), 1 = bf16, 2 = fp16 hidden-layer
+ * operands (weights and activations of the 32x32 layers rounded, fp32 accumulate).
+ * Reduced precision is an approximation of the GPU MFMA paths, used only for
+ * tolerance tests. */
+static float round_bf16(float x)
+{
+    uint32_t u; memcpy(&u, &x, 4);
+    if ((u & 0x7f800000u) == 0x7f800000u) return x;
+    u = (u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u;
+    float r; memcpy(&r, &u, 4); return r;
+}
+
+static float round_fp16(float x)
+{
+    /* RNE to binary16, returned widened to float (normal range only; the hidden
+     * activations of the bundled networks stay far inside it). */
+    if (x == 0.0f || !isfinite(x)) return x;
+    float ax = fabsf(x);
+    if (ax >= 65520.0f) return x > 0 ? INFINITY : -INFINITY;
+    int e; frexpf(ax, &e);               /* ax = m * 2^e, m in [0.5,1) */
+    int shift = (e - 1 < -14) ? -14 : e - 1;  /* exponent of the leading bit */
+    float q = ldexpf(1.0f, shift - 10);  /* ulp */
+    float r = nearbyintf(ax / q) * q;    /* ax/q exact (power-of-two scale) */
+    return x < 0 ? -r : r;
+}
+
+static void mlp_point(const or_mlp *m, const float *x, float *y, float *buf0, float *buf1, int precision)
+{
+    const float *a = x;
+    float *z = buf0;
+    for (int l = 0; l < m->nlayers; ++l) {
+        int in = m->dims[l], out = m->dims[l + 1];
+        int last = (l == m->nlayers - 1);
+        int lowp = precision != 0 && in == 32 && out == 32;
+        for (int o = 0; o < out; ++o) {
+            const float *w = m->W[l] + (size_t)o * in;
+            float acc = 0.0f;
+            for (int k = 0; k < in; ++k) {
+                float wk = w[k], ak = a[k];
+                if (lowp) {
+                    wk = precision == 1 ? round_bf16(wk) : round_fp16(wk);
+                    ak = precision == 1 ? round_bf16(ak) : round_fp16(ak);
+                }
+                acc = fmaf(wk, ak, acc);
+            }
+            float v = acc + m->b[l][o];
+            if (!last) v = fmaxf(v, 0.0f);   /* ReLU; NaN -> 0 */
+            z[o] = v;
+        }
+        if (last) { for (int o = 0; o < out; ++o) y[o] = z[o]; }
+        a = z;
+        z = (z == buf0) ? buf1 : buf0;
+    }
+}
+
+/* Batched forward: X is [n][in_stride] with the first dims[0] columns used, Y is
+ * [n][dims[nlayers]].  Mirrors NeuralNetwork::forward(batch) (neuralNetwork.cpp:54). */
+int or_mlp_forward(int nlayers, const int *dims, const float *params,
+                   const float *X, long n, int in_stride, float *Y,
+                   int precision, int nthreads)
+{
+    or_mlp m;
+    if (or_mlp_init(&m, nlayers, dims, params)) return -1;
+    if (in_stride < dims[0]) return -2;
+    int out = dims[nlayers];
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        float *b0 = (float *)malloc(sizeof(float) * (size_t)m.maxw);
+        float *b1 = (float *)malloc(sizeof(float) * (size_t)m.maxw);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (long i = 0; i < n; ++i)
+            mlp_point(&m, X + (size_t)i * in_stride, Y + (size_t)i * out, b0, b1, precision);
+        free(b0); free(b1);
+    }
+    (void)nthreads;
+    return 0;
+}
+
+/* ------------------------------------------------------------ float3 math */
+
+static f3 mk3(float x, float y, float z) { f3 r = { x, y, z }; return r; }
+static f3 add3(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static f3 mul3s(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+static float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; } /* helper_math.h:1258 */
+static float length3(f3 v) { return sqrtf(dot3(v, v)); }                   /* :1291-1294 */
+static f3 normalize3(f3 v) { float inv = 1.0f / sqrtf(dot3(v, v)); return mul3s(v, inv); } /* :1309-1313 */
+static float dot4(const float *a, const float *b)                           /* :1263 */
+{
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+}
+
+static float saturatef(float x)   /* CUDA __saturatef: NaN -> 0 */
+{
+    if (!(x > 0.0f)) return 0.0f;
+    if (x > 1.0f) return 1.0f;
+    return x;
+}
+
+static int f2i_rz(float f)        /* CUDA cvt.rzi.s32.f32: NaN -> 0, saturating */
+{
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)f;
+}
+
+static unsigned f2u_rz(float f)   /* uint(x) of a value already in [0, 255] */
+{
+    return (unsigned)f;
+}
+
+/* -------------------------------------------------- deterministic tanh */
+
+/* tanh built from IEEE basic double operations only (see header). */
+static double nr_expm1_pos(double t)   /* t >= 0 */
+{
+    if (t < 0.5) {
+        /* Taylor series of expm1, 19 terms, Horner form */
+        double s = 1.0 / 121645100408832000.0; /* 1/19! */
+        static const double inv_fact[19] = {
+            1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+            1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+            1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0,
+            1.0 / 87178291200.0, 1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
+            1.0 / 355687428096000.0, 1.0 / 6402373705728000.0,
+            1.0 / 121645100408832000.0 };
+        s = inv_fact[18];
+        for (int i = 17; i >= 0; --i) s = s * t + inv_fact[i];
+        return s * t;
+    }
+    /* exp(t) = 2^k * exp(r), r = t - k ln2 with a two-part ln2 */
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    double kd = floor(t * 1.44269504088896338700 + 0.5);
+    double r = (t - kd * ln2_hi) - kd * ln2_lo;
+    double e = 1.0 / 6402373705728000.0; /* 1/18! */
+    static const double c[18] = {
+        1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+        1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+        1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0,
+        1.0 / 87178291200.0, 1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
+        1.0 / 355687428096000.0 };
+    for (int i = 17; i >= 0; --i) e = e * r + c[i];
+    e = ldexp(e, (int)kd);
+    return e - 1.0;
+}
+
+float nr_tanh_f(float x)
+{
+    if (x != x) return x;
+    double ax = fabs((double)x);
+    if (ax > 9.5) return x > 0 ? 1.0f : -1.0f;
+    double em1 = nr_expm1_pos(2.0 * ax);
+    double t = em1 / (em1 + 2.0);
+    float r = (float)t;
+    return x < 0 ? -r : r;
+}
+
+/* ------------------------------------------------------------ scene SDF */
+
+enum { OR_SCENE_V1 = 0, OR_SCENE_TANH = 1 };
+
+static float sdfSphere(f3 p, float s) { return length3(p) - s; }          /* :67-71 */
+
+static float sdfOpSmoothUnion(float d1, float d2, float k)                 /* :144-149 */
+{
+    float h = saturatef((float)(0.5 + 0.5 * (double)(d2 - d1) / (double)k));
+    float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
+    return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
+}
+
+static float manySphere(f3 p, float nSDF, int frame)                       /* :176-196 */
+{
+    float s = nSDF;
+    f3 cP = p;
+    cP.y = (float)((double)cP.y - 0.6);
+    cP.z = (float)((double)cP.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+    for (int i = 0; i < 9; i++) {
+        if (i % 3 == 0) {
+            cP.y = (float)((double)cP.y + 0.4);
+            cP.x = (float)((double)p.x + 0.5);
+        }
+        s = sdfOpSmoothUnion(s, sdfSphere(cP, 0.1f), 0.01f);
+        cP.x = (float)((double)cP.x - 0.4);
+    }
+    return s;
+}
+
+static float sceneSDF(f3 p, float nSDF, int scene, int frame)              /* :217-230 */
+{
+    if (scene == OR_SCENE_TANH) return nr_tanh_f(nSDF);
+    return manySphere(p, nSDF, frame);
+}
+
+/* ------------------------------------------------------------- shading */
+
+static uint32_t rgbaFloatToInt(float r, float g, float b, float a)        /* :266-274 */
+{
+    r = saturatef(r); g = saturatef(g); b = saturatef(b); a = saturatef(a);
+    return (f2u_rz(a * 255) << 24) | (f2u_rz(b * 255) << 16) | (f2u_rz(g * 255) << 8) | f2u_rz(r * 255);
+}
+
+static uint32_t facingColor(f3 n, f3 rayDir)                               /* :380-384 */
+{
+    float d = dot3(n, mk3(-rayDir.x, -rayDir.y, -rayDir.z));
+    float ratio = (d > 0.0f) ? d : 0.0f;    /* max(0.0, float) -> fmax; NaN -> 0 */
+    return rgbaFloatToInt(ratio, ratio, ratio, 1.0f);
+}
+
+static uint32_t matCapColor(f3 normal, const float *normalMatrix,
+                            const uint32_t *matcap, int matW, int matH)   /* :387-413 */
+{
+    float v4[4] = { normal.x, normal.y, normal.z, 0.0f };
+    float ex = dot4(v4, normalMatrix + 0);
+    float ey = dot4(v4, normalMatrix + 4);
+    float ez = dot4(v4, normalMatrix + 8);
+    f3 ne = normalize3(mk3(ex, ey, ez));
+    float fuvx = (float)((double)ne.x * 0.5 + 0.5);
+    float fuvy = (float)((double)ne.y * 0.5 + 0.5);
+    int uvx = f2i_rz(fuvx * (float)(matW - 1));
+    int uvy = f2i_rz(fuvy * (float)(matH - 1));
+    /* out-of-range guard: unreachable for |ne| <= 1 + ulp, UB in the reference */
+    if (uvx > matW - 1) uvx = matW - 1;
+    if (uvy > matH - 1) uvy = matH - 1;
+    long index = (long)uvy * matW + uvx;
+    if (index < 0) return rgbaFloatToInt(0, 0, 0, 0);
+    return matcap[index];
+}
+
+/* ------------------------------------------------------------- render */
+
+typedef struct {
+    const float *inv_view;   /* 3x4 row-major (c_invViewMatrix) */
+    const float *normal;     /* 4x4 row-major (c_normalMatrix) */
+    int frame, color_type, num_inputs, scene;
+    const uint32_t *matcap; int mw, mh;
+} or_settings;
+
+static f3 mul34v(const float *M, f3 v)                                     /* :233-241 */
+{
+    return mk3(dot3(v, mk3(M[0], M[1], M[2])),
+               dot3(v, mk3(M[4], M[5], M[6])),
+               dot3(v, mk3(M[8], M[9], M[10])));
+}
+
+static int intersectSphere(f3 o, f3 d, float r, float *tnear, float *tfar) /* :199-215 */
+{
+    f3 Q = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
+    float a = dot3(d, d);
+    float b = (float)(2.0 * (double)dot3(Q, d));
+    float c = dot3(Q, Q) - r * r;
+    float discrim = b * b - 4 * a * c;
+    if (discrim > 0) {
+        float sq = sqrtf(discrim);
+        *tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
+        *tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
+        return 1;
+    }
+    return 0;
+}
+
+/* stats[0] = ray-steps (MLP evaluations of stepping rays), stats[1] = shade
+ * evaluations (4 per coloured ray), stats[2] = host iterations executed,
+ * stats[3] = rays that hit the bounding sphere, stats[4] = coloured pixels. */
+int or_render(int nlayers, const int *dims, const float *params,
+              const float *inv_view, const float *normal, int frame,
+              int color_type, int num_inputs, int scene,
+              const uint32_t *matcap, int mw, int mh,
+              int W, int H, int max_steps, uint32_t *out, long long *stats,
+              int nthreads)
+{
+    or_mlp m;
+    if (or_mlp_init(&m, nlayers, dims, params)) return -1;
+    if (num_inputs != 3 && num_inputs != 4) return -2;
+    if (dims[0] != num_inputs || dims[nlayers] != 1) return -3;
+    if (color_type == 1 && (!matcap || mw < 1 || mh < 1)) return -4;
+    or_settings S = { inv_view, normal, frame, color_type, num_inputs, scene, matcap, mw, mh };
+    long npix = (long)W * H;
+    long long st[5] = { 0, 0, 0, 0, 0 };
+    if (npix <= 0) { if (stats) memcpy(stats, st, sizeof st); return 0; }
+
+    unsigned *mask = (unsigned *)calloc(npix, sizeof(unsigned));
+    unsigned *idmap = (unsigned *)calloc(npix, sizeof(unsigned));
+    float *points = (float *)calloc(npix * 3, sizeof(float));
+    float *ray = (float *)calloc(npix * 3, sizeof(float));
+    float *far_ = (float *)calloc(npix, sizeof(float));
+    float *batch = (float *)calloc((size_t)npix * num_inputs * COLOR_MASK_VAL, sizeof(float));
+    float *sdf = (float *)calloc((size_t)npix * COLOR_MASK_VAL, sizeof(float));
+    if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf) {
+        free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf);
+        return -5;
+    }
+    for (long i = 0; i < npix; ++i) out[i] = 0;   /* caller's cudaMemset (main.cpp:408) */
+
+    /* initMarcher :293-358 */
+    f3 origin = mk3(dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 0),
+                    dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 4),
+                    dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 8));
+    for (int y = 0; y < H; ++y)
+        for (int x = 0; x < W; ++x) {
+            long id = (long)y * W + x;
+            float u = ((float)x / (float)W) * 2.0f - 1.0f;
+            float v = ((float)y / (float)H) * 2.0f - 1.0f;
+            f3 d = normalize3(mk3(u, v, -2.0f));
+            d = mul34v(inv_view, d);
+            float tnear, tfar;
+            if (!intersectSphere(origin, d, 1.2f, &tnear, &tfar)) {
+                mask[id] = 0; out[id] = 0; continue;
+            }
+            if (tnear < 0.0f) tnear = 0.0f;
+            f3 p = add3(origin, mul3s(d, tnear));
+            points[3 * id] = p.x; points[3 * id + 1] = p.y; points[3 * id + 2] = p.z;
+            ray[3 * id] = d.x; ray[3 * id + 1] = d.y; ray[3 * id + 2] = d.z;
+            far_[id] = tfar;
+            mask[id] = 1;
+            st[3]++;
+        }
+
+    const int ni = num_inputs;
+    for (int it = 0; it <= max_steps; ++it) {
+        /* formatInferenceReqs :549-576 -- exclusive scan; the total includes the
+         * last pixel's mask (Q1 fixed) */
+        unsigned run = 0;
+        long nstep = 0, nshade = 0;
+        for (long i = 0; i < npix; ++i) {
+            idmap[i] = run; run += mask[i];
+            if (mask[i] == 1) nstep++; else if (mask[i] >= COLOR_MASK_VAL) nshade++;
+        }
+        long batchSize = run;
+        if (it == max_steps || batchSize == 0) break;  /* for (i < MAX_STEPS) / break :652-657 */
+        /* createBatch :504-547 */
+        for (long i = 0; i < npix; ++i) {
+            unsigned mv = mask[i];
+            if (mv == 0) continue;
+            size_t bi = (size_t)idmap[i] * ni;
+            if (mv == 1) {
+                batch[bi] = points[3 * i]; batch[bi + 1] = points[3 * i + 1]; batch[bi + 2] = points[3 * i + 2];
+                if (ni == 4) batch[bi + 3] = (float)frame;
+            } else {
+                for (unsigned q = 0; q < mv; ++q) {
+                    size_t o = bi + (size_t)q * ni;
+                    batch[o] = points[3 * i] + TET[3 * q] * NORMAL_EPSILON;
+                    batch[o + 1] = points[3 * i + 1] + TET[3 * q + 1] * NORMAL_EPSILON;
+                    batch[o + 2] = points[3 * i + 2] + TET[3 * q + 2] * NORMAL_EPSILON;
+                    if (ni == 4) batch[o + 3] = (float)frame;
+                }
+            }
+        }
+        st[0] += nstep; st[1] += 4 * nshade; st[2]++;
+        long long shaded = 0;
+        /* nn.forward(batch) :661 */
+        or_mlp_forward(nlayers, dims, params, batch, batchSize, ni, sdf, 0, nthreads);
+        /* singleMarch :416-477 */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : omp_get_max_threads()) reduction(+:shaded)
+#endif
+        for (long id = 0; id < npix; ++id) {
+            unsigned mv = mask[id];
+            if (mv == 0) continue;
+            unsigned idx = idmap[id];
+            f3 d = mk3(ray[3 * id], ray[3 * id + 1], ray[3 * id + 2]);
+            f3 p = mk3(points[3 * id], points[3 * id + 1], points[3 * id + 2]);
+            if (mv >= COLOR_MASK_VAL) {
+                /* surfaceNormal :361-377 */
+                f3 acc;
+                for (int q = 0; q < 4; ++q) {
+                    f3 tp = mk3(TET[3 * q], TET[3 * q + 1], TET[3 * q + 2]);
+                    f3 pq = add3(p, mul3s(tp, NORMAL_EPSILON));
+                    f3 c = mul3s(tp, sceneSDF(pq, sdf[idx + q], S.scene, S.frame));
+                    acc = (q == 0) ? c : add3(acc, c);
+                }
+                f3 n = normalize3(acc);
+                out[id] = (S.color_type == 0) ? facingColor(n, d)
+                                              : matCapColor(n, S.normal, S.matcap, S.mw, S.mh);
+                mask[id] = 0;
+                shaded++;
+                continue;
+            }
+            float tstep = sceneSDF(p, sdf[idx], S.scene, S.frame);
+            far_[id] -= tstep;
+            if (far_[id] <= 0) { mask[id] = 0; out[id] = 0; continue; }
+            p = add3(p, mul3s(d, tstep));
+            points[3 * id] = p.x; points[3 * id + 1] = p.y; points[3 * id + 2] = p.z;
+            if (tstep < MARCHING_EPSILON) mask[id] = COLOR_MASK_VAL;
+        }
+        st[4] += shaded;
+    }
+    if (stats) memcpy(stats, st, sizeof st);
+    free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf);
+    return 0;
+}
+
+/* Scene SDF on its own, for unit tests of the step arithmetic. */
+float or_scene_sdf(float px, float py, float pz, float nsdf, int scene, int frame)
+{
+    return sceneSDF(mk3(px, py, pz), nsdf, scene, frame);
+}

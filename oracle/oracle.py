@@ -1,0 +1,94 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product package.  See nr_oracle.c for what it
+restates and how it is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "_build", "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(SO):
+            build()
+        L = ctypes.CDLL(SO)
+        P = ctypes.c_void_p
+        I = ctypes.c_int
+        L.or_mlp_forward.restype = I
+        L.or_mlp_forward.argtypes = [I, P, P, P, ctypes.c_long, I, P, I, I]
+        L.or_render.restype = I
+        L.or_render.argtypes = [I, P, P, P, P, I, I, I, I, P, I, I, I, I, I, P, P, I]
+        L.or_scene_sdf.restype = ctypes.c_float
+        L.or_scene_sdf.argtypes = [ctypes.c_float] * 4 + [I, I]
+        L.nr_tanh_f.restype = ctypes.c_float
+        L.nr_tanh_f.argtypes = [ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def pack_params(kernels, biases):
+    """Keras kernels (in, out) -> the oracle's out-major W[out][in] + bias per layer
+    (DenseLayer::initializeWeights, denseLayer.cu:217-227)."""
+    parts = []
+    dims = [kernels[0].shape[0]]
+    for K, b in zip(kernels, biases):
+        K = np.asarray(K, np.float32)
+        parts.append(np.ascontiguousarray(K.T).reshape(-1))
+        parts.append(np.asarray(b, np.float32).reshape(-1))
+        dims.append(K.shape[1])
+    return np.array(dims, np.int32), np.concatenate(parts).astype(np.float32)
+
+
+class OracleNet:
+    def __init__(self, kernels, biases):
+        self.dims, self.params = pack_params(kernels, biases)
+        self.nlayers = len(kernels)
+
+    def forward(self, X, precision=0, nthreads=0):
+        X = np.ascontiguousarray(X, np.float32)
+        n = X.shape[0]
+        Y = np.zeros((n, int(self.dims[-1])), np.float32)
+        rc = lib().or_mlp_forward(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, X.ctypes.data, n,
+                                  X.shape[1], Y.ctypes.data, precision, nthreads)
+        assert rc == 0, rc
+        return Y
+
+    def render(self, W, H, inv_view, normal, frame=0, color_type=0, num_inputs=3, scene=0, matcap=None,
+               max_steps=6000, nthreads=0):
+        out = np.zeros((H, W), np.uint32)
+        stats = np.zeros(5, np.int64)
+        iv = np.ascontiguousarray(inv_view, np.float32)
+        nm = np.ascontiguousarray(normal, np.float32)
+        if matcap is not None:
+            mc = np.ascontiguousarray(matcap, np.uint32)
+            mp, mw, mh = mc.ctypes.data, mc.shape[1], mc.shape[0]
+        else:
+            mc, mp, mw, mh = None, None, 0, 0
+        rc = lib().or_render(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, iv.ctypes.data,
+                             nm.ctypes.data, frame, color_type, num_inputs, scene, mp, mw, mh, W, H, max_steps,
+                             out.ctypes.data, stats.ctypes.data, nthreads)
+        assert rc == 0, rc
+        keys = ["ray_steps", "shade_evals", "iterations", "rays_hit", "rays_shaded"]
+        return out, dict(zip(keys, (int(v) for v in stats)))
+
+
+def scene_sdf(p, nsdf, scene=0, frame=0):
+    return lib().or_scene_sdf(float(p[0]), float(p[1]), float(p[2]), float(nsdf), scene, frame)
+
+
+def tanh_f(x):
+    return lib().nr_tanh_f(float(x))

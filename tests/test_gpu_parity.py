@@ -1,0 +1,184 @@
+"""GPU parity: libnr.so (HIP, gfx950) against the CPU oracle, through the C ABI.
+
+FP32 is bit-exact by contract (DESIGN.md "numerics"); bf16/fp16 are tolerance
+tests.  Pixel (W-1, H-1) needs no exclusion here: both sides fix quirk Q1.
+"""
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+from conftest import GEOMS
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rend():
+    r = nr.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def chrome():
+    return nr.load_png(nr.matcap_path("Chrome"))
+
+
+def pts(n, seed=0, lo=-1.2, hi=1.2):
+    return np.random.default_rng(seed).uniform(lo, hi, size=(n, 3)).astype(np.float32)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_mlp_forward_bitexact(rend, nets, golden, geom):
+    dims, K, B = nets[geom]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    X = golden["kat"]["X"]
+    y_gpu = rend.mlp_forward(X)
+    y_cpu = oracle.OracleNet(K, B).forward(X)
+    assert np.array_equal(y_gpu.view(np.uint32), y_cpu.view(np.uint32)), \
+        f"{(y_gpu != y_cpu).sum()} of {len(X)} differ, max {np.abs(y_gpu - y_cpu).max()}"
+
+
+@pytest.mark.parametrize("n", [1, 31, 64, 65, 1000, 100003])
+def test_mlp_forward_ragged(rend, nets, n):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    X = pts(n, seed=n)
+    assert np.array_equal(rend.mlp_forward(X), oracle.OracleNet(K, B).forward(X))
+
+
+def test_simpleinfer_batch_consistency(rend, nets):
+    # simpleInfer.cpp:112-147: 1e6 identical zero inputs -> all outputs equal
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    Y = rend.mlp_forward(np.zeros((1000000, 3), np.float32))
+    assert (Y == Y[0]).all()
+    assert Y[0, 0] == oracle.OracleNet(K, B).forward(np.zeros((1, 3), np.float32))[0, 0]
+
+
+@pytest.mark.parametrize("layer", range(9))
+def test_layer_forward_bitexact(rend, nets, layer):
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B)
+    A = np.random.default_rng(layer).uniform(-1, 1, size=(777, dims[layer])).astype(np.float32)
+    Z = rend.layer_forward(layer, A)
+    net1 = oracle.OracleNet([K[layer]], [B[layer]])
+    ref = net1.forward(A)
+    if layer != 8:
+        ref = np.maximum(ref, 0)  # single-layer oracle net treats its only layer as last (linear)
+    assert np.array_equal(Z, ref)
+
+
+RENDER_CASES = [
+    # W, H, scene, color, rx, ry, zoom, steps
+    (128, 128, "v1", "matcap", 0.0, 0.0, 2.0, 128),
+    (128, 96, "tanh", "matcap", -18.3, 150.7, 2.25, 256),
+    (97, 61, "v1", "facing", 25.0, 40.0, 2.0, 64),
+    (64, 64, "v1", "facing", 10.0, 300.0, 3.0, 6000),
+    (1, 1, "v1", "facing", 0.0, 0.0, 2.0, 100),
+]
+
+
+@pytest.mark.parametrize("W,H,scene,color,rx,ry,zoom,steps", RENDER_CASES)
+def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, steps):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(rx, ry, zoom)
+    ct = nr.NR_COLOR_MATCAP if color == "matcap" else nr.NR_COLOR_FACING
+    rend.set_view(iv, nm, 0).set_static(ct, 3).set_scene(scene).set_matcap(chrome)
+    img, st = rend.render(W, H, steps)
+    ref, rst = oracle.OracleNet(K, B).render(W, H, iv, nm, color_type=ct, scene=0 if scene == "v1" else 1,
+                                             matcap=chrome if ct else None, max_steps=steps)
+    diff = img != ref
+    assert not diff.any(), f"{diff.sum()} pixels differ; gpu stats {st} oracle {rst}"
+    for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
+        assert st[k] == rst[k], (k, st, rst)
+
+
+@pytest.mark.parametrize("geom", ["plane_2", "car_1", "plane_3", "3a3d4a90a2db90b4203936772104a82d.obj"])
+def test_render_geometries(rend, nets, chrome, geom):
+    dims, K, B = nets[geom]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(-20.0, 35.0, 2.0)
+    rend.set_view(iv, nm, 7).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+    img, st = rend.render(80, 72, 128)
+    ref, rst = oracle.OracleNet(K, B).render(80, 72, iv, nm, frame=7, color_type=1, matcap=chrome, max_steps=128)
+    assert np.array_equal(img, ref)
+    assert st["ray_steps"] == rst["ray_steps"]
+
+
+def test_render_empty_scene(rend, nets):
+    # eye at (0, 0, 5) looking along +z, away from the bounding sphere: every ray misses
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B)
+    iv = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, -1, 5], np.float32)
+    nm = np.array([1, 0, 0, 0, 0, 1, 0, 0, 0, 0, -1, 5, 0, 0, 0, 1], np.float32)
+    rend.set_view(iv, nm).set_static(0, 3).set_scene("v1")
+    img, st = rend.render(64, 48, 100)
+    ref, rst = oracle.OracleNet(K, B).render(64, 48, iv, nm, max_steps=100)
+    assert (img == 0).all() and (ref == 0).all()
+    # the line through the eye still crosses the sphere behind it: those rays "hit" with
+    # tnear, tfar < 0 and die on their first step (tfar <= 0), exactly as in the reference
+    for k in ("rays_hit", "ray_steps", "rays_shaded", "iterations"):
+        assert st[k] == rst[k], (k, st, rst)
+    assert st["rays_shaded"] == 0
+
+
+def test_render_zero_steps(rend, nets):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B)
+    iv, nm = nr.camera(0, 0, 2)
+    rend.set_view(iv, nm).set_static(0, 3).set_scene("v1")
+    img, st = rend.render(32, 32, 0)
+    assert (img == 0).all() and st["ray_steps"] == 0 and st["rays_hit"] == 32 * 32
+
+
+@pytest.mark.parametrize("nshards,band", [(2, 8), (3, 5), (8, 8), (4, 1)])
+def test_shards_assemble_to_frame(rend, nets, chrome, nshards, band):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(-10.0, 20.0, 2.0)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    W, H = 70, 83
+    full, _ = rend.render(W, H, 128)
+    shards = [rend.render_shard(W, H, band, nshards, s, 128)[0] for s in range(nshards)]
+    assert sum(s.shape[0] for s in shards) == H
+    assert np.array_equal(nr.assemble_shards(shards, W, H, band, nshards), full)
+
+
+@pytest.mark.parametrize("prec,tol", [("bf16", 0.05), ("fp16", 0.01)])
+def test_mlp_lowp_tolerance(rend, nets, golden, prec, tol):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec)
+    X = golden["kat"]["X"]
+    y = rend.mlp_forward(X)[:, 0]
+    y64 = golden["kat"]["plane_1"]
+    # tolerance relative to the output scale (SDF range of the bundled nets ~[-0.3, 1])
+    assert np.abs(y - y64).max() < tol, np.abs(y - y64).max()
+    rend.set_precision("fp32")
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_render_lowp_close(rend, nets, chrome, prec):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec)
+    iv, nm = nr.camera(0, 0, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    img, st = rend.render(128, 128, 128)
+    ref, rst = oracle.OracleNet(K, B).render(128, 128, iv, nm, color_type=1, matcap=chrome, max_steps=128)
+    fg, fg_ref = img != 0, ref != 0
+    iou = (fg & fg_ref).sum() / max((fg | fg_ref).sum(), 1)
+    assert iou > 0.97, iou
+    assert abs(st["ray_steps"] - rst["ray_steps"]) / rst["ray_steps"] < 0.05
+    rend.set_precision("fp32")
+
+
+def test_render_deterministic(rend, nets, chrome):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(0, 0, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    a, sa = rend.render(1024, 1024, 128)
+    b, sb = rend.render(1024, 1024, 128)
+    assert np.array_equal(a, b) and sa["ray_steps"] == sb["ray_steps"]
