@@ -15,6 +15,7 @@ NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}
 NR_SCENE = {"v1": 0, "tanh": 1}
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
+NR_SCHEDULE = {"persistent": 0, "wavefront": 1}
 
 # every symbol include/neural_render.h declares
 EXPORTS = [
@@ -23,7 +24,7 @@ EXPORTS = [
     "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_shard_rows",
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
-    "nr_set_poll_interval",
+    "nr_set_poll_interval", "nr_set_schedule",
 ]
 
 
@@ -107,6 +108,7 @@ def lib():
         "nr_set_profiling": (I, [P, I]),
         "nr_prof_collect": (I, [P, ctypes.POINTER(NRKernelProf)]),
         "nr_set_poll_interval": (I, [P, I]),
+        "nr_set_schedule": (I, [P, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -35,10 +35,13 @@ struct nr_ctx {
     std::vector<float *> d_W, d_b;                     // out-major per layer (generic kernel)
     bool fused = false;
     int precision = NR_PRECISION_FP32;
-    float *d_pack32 = nullptr;
-    uint16_t *d_lp = nullptr;
-    float *d_lpf = nullptr;
-    MlpArgs mlp{};
+    float *d_pack32 = nullptr, *d_pack16 = nullptr;
+    uint16_t *d_lp = nullptr, *d_lp16 = nullptr;
+    float *d_lpf = nullptr, *d_lpf16 = nullptr;
+    MlpArgs mlp{};    // 32-point tiles: k_mlp, k_march, k_shade (wavefront schedule)
+    MlpArgs mlp16{};  // 16-point tiles: k_trace, k_shade16 (persistent schedule)
+    int schedule = 0; // NR_SCHED_PERSISTENT
+    uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
 
     // settings
     float inv_view[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 2};
@@ -98,27 +101,39 @@ int free_network(nr_ctx *c) {
     for (auto *p : c->d_b) (void)hipFree(p);
     c->d_W.clear(); c->d_b.clear();
     dfree(c->d_pack32); dfree(c->d_lp); dfree(c->d_lpf);
+    dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16);
     c->fused = false;
     return NR_OK;
 }
 
+int upload_pack(nr_ctx *c, const std::vector<uint16_t> &a, const std::vector<float> &f, uint16_t *&d_a, float *&d_f,
+                MlpArgs &M) {
+    std::vector<uint16_t> aa(a);
+    std::vector<float> ff(f);
+    size_t ab = (aa.size() * 2 + 15) / 16 * 16, fb = (ff.size() * 4 + 15) / 16 * 16;
+    aa.resize(ab / 2, 0); ff.resize(fb / 4, 0.0f);
+    HIPCHK(c, hipMalloc(&d_a, ab));
+    HIPCHK(c, hipMalloc(&d_f, fb));
+    HIPCHK(c, hipMemcpy(d_a, aa.data(), ab, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d_f, ff.data(), fb, hipMemcpyHostToDevice));
+    M.lp = d_a; M.lpf = d_f;
+    M.lp_bytes = (int)ab; M.lpf_bytes = (int)fb;
+    return NR_OK;
+}
+
 int upload_lowp(nr_ctx *c) {
-    dfree(c->d_lp); dfree(c->d_lpf);
-    c->mlp.lp = nullptr; c->mlp.lpf = nullptr; c->mlp.lp_bytes = 0; c->mlp.lpf_bytes = 0;
+    dfree(c->d_lp); dfree(c->d_lpf); dfree(c->d_lp16); dfree(c->d_lpf16);
+    for (MlpArgs *M : {&c->mlp, &c->mlp16}) { M->lp = nullptr; M->lpf = nullptr; M->lp_bytes = 0; M->lpf_bytes = 0; }
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
     if (!pack_lowp(c->dims, c->kernels, c->biases, c->precision, a, f))
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
-    size_t ab = (a.size() * 2 + 15) / 16 * 16, fb = (f.size() * 4 + 15) / 16 * 16;
-    a.resize(ab / 2, 0); f.resize(fb / 4, 0.0f);
-    HIPCHK(c, hipMalloc(&c->d_lp, ab));
-    HIPCHK(c, hipMalloc(&c->d_lpf, fb));
-    HIPCHK(c, hipMemcpy(c->d_lp, a.data(), ab, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->d_lpf, f.data(), fb, hipMemcpyHostToDevice));
-    c->mlp.lp = c->d_lp; c->mlp.lpf = c->d_lpf;
-    c->mlp.lp_bytes = (int)ab; c->mlp.lpf_bytes = (int)fb;
-    return NR_OK;
+    int rc = upload_pack(c, a, f, c->d_lp, c->d_lpf, c->mlp);
+    if (rc != NR_OK) return rc;
+    if (!pack_lowp_16(c->dims, c->kernels, c->biases, c->precision, a, f))
+        return set_err(c, NR_E_INVALID, "low-precision pack failed");
+    return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
 }
 
 int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>> K, std::vector<std::vector<float>> B) {
@@ -139,18 +154,24 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
         HIPCHK(c, hipMemcpy(dw, W.data(), W.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(db, c->biases[l].data(), (size_t)out * 4, hipMemcpyHostToDevice));
     }
-    std::vector<float> pack;
-    c->fused = pack_fp32(c->dims, c->kernels, c->biases, pack);
+    std::vector<float> pack, pack16;
+    c->fused = pack_fp32(c->dims, c->kernels, c->biases, pack) &&
+               pack_fp32_16(c->dims, c->kernels, c->biases, pack16);
     c->mlp = MlpArgs{};
+    c->mlp16 = MlpArgs{};
     if (c->fused) {
         size_t pb = (pack.size() * 4 + 15) / 16 * 16;
         pack.resize(pb / 4, 0.0f);
+        pack16.resize(pb / 4, 0.0f);
         HIPCHK(c, hipMalloc(&c->d_pack32, pb));
         HIPCHK(c, hipMemcpy(c->d_pack32, pack.data(), pb, hipMemcpyHostToDevice));
-        c->mlp.pack32 = c->d_pack32;
-        c->mlp.pack32_bytes = (int)pb;
-        c->mlp.in0 = c->dims[0];
-        c->mlp.nh = nl - 2;
+        HIPCHK(c, hipMalloc(&c->d_pack16, pb));
+        HIPCHK(c, hipMemcpy(c->d_pack16, pack16.data(), pb, hipMemcpyHostToDevice));
+        c->mlp.pk = c->d_pack32;
+        c->mlp16.pk = c->d_pack16;
+        c->mlp.pk_bytes = c->mlp16.pk_bytes = (int)pb;
+        c->mlp.in0 = c->mlp16.in0 = c->dims[0];
+        c->mlp.nh = c->mlp16.nh = nl - 2;
     }
     return upload_lowp(c);
 }
@@ -252,7 +273,7 @@ int nr_destroy(nr_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_io); dfree(c->d_matcap);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -400,21 +421,63 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
     memcpy(A.inv_view, c->inv_view, sizeof A.inv_view);
     memcpy(A.normal, c->normal, sizeof A.normal);
+    hipStream_t s = c->stream;
+    int cus = num_cus(c->device);
+    int rc2;
+    if (c->schedule == NR_SCHED_PERSISTENT) {
+        // 8 shard counters on their own 128-byte lines, then 4 x u64 stats
+        const size_t tr_bytes = 8 * 128 + 4 * 8;
+        if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, tr_bytes));
+        TraceArgs T{};
+        T.pix_ctr = c->d_tr;
+        T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + 8 * 32);
+        T.shade_p = c->d_SP;
+        T.shade_d = c->d_SD;
+        HIPCHK(c, hipEventRecord(c->ev0, s));
+        HIPCHK(c, hipMemsetAsync(c->d_tr, 0, tr_bytes, s));
+        int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * 4);
+        if (grid < 1) grid = 1;
+        if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
+        HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
+        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        if ((rc2 = prof_begin(c, 2, s)) != NR_OK) return rc2;
+        HIPCHK(c, launch_shade16(A, c->mlp16, T, grid, s));
+        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        if (c->profiling) c->prof_renders++;
+        HIPCHK(c, hipEventRecord(c->ev1, s));
+        if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
+        if (stats) {
+            unsigned long long hs[4];
+            HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            st.ray_steps = hs[0];
+            st.rays_hit = hs[1];
+            st.iterations = (int32_t)hs[2];
+            st.rays_shaded = hs[3];
+            st.shade_evals = 4ull * hs[3];
+            st.launches = 3;
+            float ms = 0;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+            st.ms_total = ms;
+            *stats = st;
+        } else if (loc != NR_DEVICE) {
+            HIPCHK(c, hipStreamSynchronize(s));
+        }
+        return NR_OK;
+    }
+    // ---- wavefront schedule: one k_march launch per iteration
     // counters: [0, max_steps] live counts, [max_steps+1] shade count, [max_steps+2 ...] shade_it
     uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + max_steps + 1, *shade_it = c->d_ctr + max_steps + 2;
     size_t nctr = (size_t)2 * max_steps + 2;
-    hipStream_t s = c->stream;
     HIPCHK(c, hipEventRecord(c->ev0, s));
     HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, nctr * 4, s));
     QueueArgs Q{};
     Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
     Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
-    int rc2;
     if ((rc2 = prof_begin(c, 0, s)) != NR_OK) return rc2;
     HIPCHK(c, launch_init(A, Q, s));
     if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
     int launches = 2;
-    int cus = num_cus(c->device);
     int march_grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * 4);
     if (march_grid < 1) march_grid = 1;
     for (int it = 0; it < max_steps; ++it) {
@@ -572,6 +635,14 @@ int nr_prof_collect(nr_ctx *c, nr_kernel_prof *out) {
     c->recs.clear();
     c->prof_renders = 0;
     *out = p;
+    return NR_OK;
+}
+
+int nr_set_schedule(nr_ctx *c, int schedule) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    if (schedule != NR_SCHED_PERSISTENT && schedule != NR_SCHED_WAVEFRONT)
+        return set_err(c, NR_E_INVALID, "unknown schedule %d", schedule);
+    c->schedule = schedule;
     return NR_OK;
 }
 

@@ -1,0 +1,187 @@
+// nr_device.h -- device-side building blocks shared by the march kernels
+// (nr_kernels.hip: wavefront schedule, nr_trace.hip: persistent schedule).
+//
+// Restatement of the reference device helpers (helper_math.h:1248-1313,
+// volumeRender_kernel.cu:38-61, :67-275, :361-413); the expression-by-expression
+// float/double promotions mirror the CUDA source (double literals promote) and are
+// kept in lock-step with oracle/nr_oracle.c.  Compiled with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nr_internal.h"
+#include "nr_kernels.h"
+
+namespace nr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// ------------------------------------------------------------------ float math
+// Restatement of the reference device helpers (helper_math.h:1248-1313,
+// volumeRender_kernel.cu:67-275); the expression-by-expression promotions mirror
+// the CUDA source (double literals promote).  Kept in lock-step with the oracle.
+
+struct F3 { float x, y, z; };
+__device__ __forceinline__ F3 mk3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ F3 add3(F3 a, F3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 mul3s(F3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float dot3(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float length3(F3 v) { return sqrtf(dot3(v, v)); }
+__device__ __forceinline__ F3 normalize3(F3 v) { float inv = 1.0f / sqrtf(dot3(v, v)); return mul3s(v, inv); }
+__device__ __forceinline__ float dot4(float a0, float a1, float a2, float a3, const float *b) {
+    return a0 * b[0] + a1 * b[1] + a2 * b[2] + a3 * b[3];
+}
+__device__ __forceinline__ float saturatef_(float x) {
+    if (!(x > 0.0f)) return 0.0f;
+    if (x > 1.0f) return 1.0f;
+    return x;
+}
+__device__ __forceinline__ int f2i_rz(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)f;
+}
+
+static __constant__ float c_tet[12] = {1, -1, -1, -1, -1, 1, -1, 1, -1, 1, 1, 1};  // :38-43
+#define NORMAL_EPSILON 0.00001f
+#define MARCHING_EPSILON 0.000001f
+
+// tanh from IEEE basic double operations (identical algorithm to the oracle).
+__device__ double expm1_pos(double t) {
+    if (t < 0.5) {
+        const double inv_fact[19] = {
+            1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+            1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+            1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0,
+            1.0 / 87178291200.0, 1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
+            1.0 / 355687428096000.0, 1.0 / 6402373705728000.0,
+            1.0 / 121645100408832000.0};
+        double s = inv_fact[18];
+#pragma unroll
+        for (int i = 17; i >= 0; --i) s = s * t + inv_fact[i];
+        return s * t;
+    }
+    const double ln2_hi = 6.93147180369123816490e-01;
+    const double ln2_lo = 1.90821492927058770002e-10;
+    double kd = floor(t * 1.44269504088896338700 + 0.5);
+    double r = (t - kd * ln2_hi) - kd * ln2_lo;
+    const double c[18] = {
+        1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+        1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+        1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0,
+        1.0 / 87178291200.0, 1.0 / 1307674368000.0, 1.0 / 20922789888000.0,
+        1.0 / 355687428096000.0};
+    double e = 1.0 / 6402373705728000.0;
+#pragma unroll
+    for (int i = 17; i >= 0; --i) e = e * r + c[i];
+    e = ldexp(e, (int)kd);
+    return e - 1.0;
+}
+
+__device__ float nr_tanh(float x) {
+    if (x != x) return x;
+    double ax = fabs((double)x);
+    if (ax > 9.5) return x > 0 ? 1.0f : -1.0f;
+    double em1 = expm1_pos(2.0 * ax);
+    double t = em1 / (em1 + 2.0);
+    float r = (float)t;
+    return x < 0 ? -r : r;
+}
+
+__device__ __forceinline__ float smooth_union(float d1, float d2, float k) {  // :144-149
+    // h = __saturatef(0.5 + 0.5*(d2-d1)/k).  When |d2-d1| >= k the double quotient is
+    // >= 0.5 in magnitude (division and rounding are monotone, 0.5 is representable), so
+    // the saturated h is exactly 1 or 0 and the f64 division can be skipped bit-exactly.
+    const float t = d2 - d1;
+    float h;
+    if (t >= k) h = 1.0f;
+    else if (t <= -k) h = 0.0f;
+    else h = saturatef_((float)(0.5 + 0.5 * (double)t / (double)k));
+    float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
+    return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
+}
+
+__device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
+    float s = nsdf;
+    F3 cP = p;
+    cP.y = (float)((double)cP.y - 0.6);
+    cP.z = (float)((double)cP.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        if (i % 3 == 0) {
+            cP.y = (float)((double)cP.y + 0.4);
+            cP.x = (float)((double)p.x + 0.5);
+        }
+        s = smooth_union(s, length3(cP) - 0.1f, 0.01f);
+        cP.x = (float)((double)cP.x - 0.4);
+    }
+    return s;
+}
+
+__device__ __forceinline__ float scene_sdf(F3 p, float nsdf, int scene, int frame) {  // :217-230
+    if (scene == NR_SCENE_TANH) return nr_tanh(nsdf);
+    return many_sphere(p, nsdf, frame);
+}
+
+__device__ __forceinline__ uint32_t rgba_to_uint(float r, float g, float b, float a) {  // :266-274
+    r = saturatef_(r); g = saturatef_(g); b = saturatef_(b); a = saturatef_(a);
+    return ((uint32_t)(a * 255) << 24) | ((uint32_t)(b * 255) << 16) | ((uint32_t)(g * 255) << 8) |
+           (uint32_t)(r * 255);
+}
+
+__device__ uint32_t shade_color(const RenderArgs &A, F3 n, F3 d) {
+    if (A.color_type == NR_COLOR_FACING) {  // facingColor :380-384
+        float dd = dot3(n, mk3(-d.x, -d.y, -d.z));
+        float ratio = (dd > 0.0f) ? dd : 0.0f;
+        return rgba_to_uint(ratio, ratio, ratio, 1.0f);
+    }
+    // matCapColor :387-413
+    float ex = dot4(n.x, n.y, n.z, 0.0f, A.normal + 0);
+    float ey = dot4(n.x, n.y, n.z, 0.0f, A.normal + 4);
+    float ez = dot4(n.x, n.y, n.z, 0.0f, A.normal + 8);
+    F3 ne = normalize3(mk3(ex, ey, ez));
+    float fuvx = (float)((double)ne.x * 0.5 + 0.5);
+    float fuvy = (float)((double)ne.y * 0.5 + 0.5);
+    int uvx = f2i_rz(fuvx * (float)(A.mw - 1));
+    int uvy = f2i_rz(fuvy * (float)(A.mh - 1));
+    if (uvx > A.mw - 1) uvx = A.mw - 1;
+    if (uvy > A.mh - 1) uvy = A.mh - 1;
+    long index = (long)uvy * A.mw + uvx;
+    if (index < 0) return 0u;
+    return A.matcap[index];
+}
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// Position of the d-th (0-based) set bit of m (m must have more than d bits set).
+__device__ __forceinline__ int select_bit(uint64_t m, int d) {
+    int lo = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {
+        uint64_t below = m & ((1ull << (lo + step)) - 1ull);
+        if (__popcll(below) <= d) lo += step;
+    }
+    return lo;
+}
+
+// Exclusive position of this lane among the set lanes of `pred`, and one atomic per wave.
+__device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t *counter) {
+    uint64_t m = __ballot(pred);
+    uint32_t cnt = (uint32_t)__popcll(m);
+    if (cnt == 0) return 0;
+    int lane = lane_id();
+    int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, cnt);
+    base = __shfl(base, leader);
+    uint64_t below = m & ((1ull << lane) - 1ull);
+    return base + (uint32_t)__popcll(below);
+}
+
+}  // namespace nr

@@ -48,6 +48,12 @@ bool fused_shape_ok(const std::vector<int> &dims);
 // Keras kernels (in x out, row-major) -> packs.  Returns false if shape unsupported.
 bool pack_fp32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
+// 16-point-tile layouts (v_mfma_f32_16x16x4_f32 / 16x16x32), same sizes as the above.
+bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+                  const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
+bool pack_lowp_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+                  const std::vector<std::vector<float>> &biases, int precision,
+                  std::vector<uint16_t> &a_ops, std::vector<float> &bias);
 bool pack_lowp(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                const std::vector<std::vector<float>> &biases, int precision,
                std::vector<uint16_t> &a_ops, std::vector<float> &bias);

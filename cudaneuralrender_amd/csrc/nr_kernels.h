@@ -7,10 +7,10 @@ namespace nr {
 
 // Network packs resident in device memory, staged into LDS by every block.
 struct MlpArgs {
-    const float *pack32;    // fp32 pack (nr_internal.h PK_*)
+    const float *pk;        // fp32 pack (nr_internal.h PK_*; 32- or 16-wide layout)
     const uint16_t *lp;     // bf16/fp16 A operands (precision != fp32)
     const float *lpf;       // float side of the low-precision pack
-    int pack32_bytes, lp_bytes, lpf_bytes;
+    int pk_bytes, lp_bytes, lpf_bytes;
     int in0, nh;
 };
 
@@ -37,6 +37,14 @@ struct QueueArgs {
     uint32_t *shade_it;     // per-iteration count of waves that enqueued converged rays
 };
 
+// Persistent-schedule state (nr_trace.hip).
+struct TraceArgs {
+    uint32_t *pix_ctr;          // 8 pixel-queue shard counters, one per 128-byte line (stride 32)
+    unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded
+    float4 *shade_p;            // per local pixel: converged point, w = 1 if it must be coloured
+    float4 *shade_d;            // per local pixel: ray direction
+};
+
 int smem_bytes(const MlpArgs &M, int prec);
 hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
 hipError_t launch_dense(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
@@ -45,6 +53,8 @@ hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st);
 hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int prec, int it, int grid,
                         hipStream_t st);
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
+hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
+hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);
 

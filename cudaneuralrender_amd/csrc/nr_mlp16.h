@@ -1,0 +1,215 @@
+// nr_mlp16.h -- the MLP on 16-point MFMA tiles (v_mfma_f32_16x16x4_f32 for fp32,
+// v_mfma_f32_16x16x32_{bf16,f16} for reduced precision).
+//
+// A wave holds 64 points, point p in lane p.  They form 4 tiles of 16 points
+// (tile t = points 16t..16t+15); inside a tile lane (j, g) = (lane & 15, lane >> 4)
+// holds point j and 8 of the 32 hidden units (group g).  Only tiles whose bit is set
+// in `tmask` are computed (wave-uniform), so a wave with few live rays pays for
+// ceil(live/16) tiles, not 4 -- the granularity that keeps the tail of the march short.
+//
+// FP32 numerics: the f32 MFMA is a k-ordered fmaf chain (cdna_hip_programming.md §3);
+// the pack (nr_pack.cpp, pack_fp32_16) permutes hidden units so that each dot product
+// runs over k = 0..31 in ascending order from +0, then adds the bias -- bit-for-bit the
+// reference dense layer as restated by the oracle (denseLayer.cu:126-176).
+#pragma once
+#include "nr_device.h"
+
+namespace nr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Broadcast of the 4 tiles' inputs: lane (j, g) of tile t needs point 16t + j.
+struct TileIn {
+    float x[4], y[4], z[4];
+};
+
+__device__ __forceinline__ TileIn tile_inputs(float x, float y, float z) {
+    const int j = lane_id() & 15;
+    TileIn T;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        T.x[t] = __shfl(x, 16 * t + j);
+        T.y[t] = __shfl(y, 16 * t + j);
+        T.z[t] = __shfl(z, 16 * t + j);
+    }
+    return T;
+}
+
+// z_t lives in lane (j, 3) = 48 + j of tile t; point p = 16t + j gets it back in lane p.
+__device__ __forceinline__ float tile_outputs(const float zt[4]) {
+    const int lane = lane_id(), j = lane & 15, t = lane >> 4;
+    float r0 = __shfl(zt[0], 48 + j), r1 = __shfl(zt[1], 48 + j);
+    float r2 = __shfl(zt[2], 48 + j), r3 = __shfl(zt[3], 48 + j);
+    return t == 0 ? r0 : (t == 1 ? r1 : (t == 2 ? r2 : r3));
+}
+
+__device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y, float z,
+                            uint32_t tmask) {
+    const int lane = lane_id(), g = lane >> 4;
+    const TileIn T = tile_inputs(x, y, z);
+    float a[4][8];
+    // layer 0 on VALU: fmaf chain over the inputs from +0, + bias, ReLU.  Register k of
+    // group g holds unit 4k + g (or 8g + k when the next layer is the final one).
+    {
+        const float4 *w0 = reinterpret_cast<const float4 *>(s + PK_L0W) + g * 8;
+        const float *b0 = s + PK_L0B + g * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float4 w = w0[k];
+            const float bk = b0[k];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (!(tmask >> t & 1u)) continue;
+                float acc = __builtin_fmaf(w.x, T.x[t], 0.0f);
+                acc = __builtin_fmaf(w.y, T.y[t], acc);
+                acc = __builtin_fmaf(w.z, T.z[t], acc);
+                if (in0 == 4) acc = __builtin_fmaf(w.w, fr, acc);
+                a[t][k] = fmaxf(acc + bk, 0.0f);
+            }
+        }
+    }
+    // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
+    for (int jl = 0; jl < nh; ++jl) {
+        const float *L = s + PK_HID + jl * PK_HID_STRIDE;
+        float4 wq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wq[q] = reinterpret_cast<const float4 *>(L)[q * 64 + lane];
+        f32x4 c[4][2];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            c[t][0] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            c[t][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int st = 0; st < 8; ++st) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int m = 2 * st + mt;
+                const float4 wv = wq[m >> 2];
+                const float w = (m & 3) == 0 ? wv.x : ((m & 3) == 1 ? wv.y : ((m & 3) == 2 ? wv.z : wv.w));
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (tmask >> t & 1u) c[t][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w, a[t][st], c[t][mt], 0, 0, 0);
+            }
+        }
+        const float4 *bb = reinterpret_cast<const float4 *>(L + 1024 + g * 8);
+        const float4 blo = bb[0], bhi = bb[1];
+        const float bias[8] = {blo.x, blo.y, blo.z, blo.w, bhi.x, bhi.y, bhi.z, bhi.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!(tmask >> t & 1u)) continue;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
+        }
+    }
+    // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
+    // groups 0 -> 1 -> 2 -> 3 with one cross-lane hand-off per group.
+    const float *wf = s + pk_final(nh) + g * 8;
+    const float bf = s[pk_final(nh) + 32];
+    float w8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w8[k] = wf[k];
+    float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (!(tmask >> t & 1u)) continue;
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(w8[k], a[t][k], acc);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+            float nacc = __shfl(acc, (lane + 48) & 63);  // from lane - 16 (group g - 1)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nacc = __builtin_fmaf(w8[k], a[t][k], nacc);
+            acc = (g == q) ? nacc : acc;
+        }
+        zt[t] = acc + bf;
+    }
+    return tile_outputs(zt);
+}
+
+// bf16 / fp16 hidden layers: one v_mfma_f32_16x16x32 per row tile per layer (K = 32
+// in a single instruction); layer 0 and the final layer in fp32 on VALU.  Register
+// k = 4mt + r of group g holds unit 16mt + 4g + r (the MFMA C layout, unpermuted).
+template <int PREC>
+__device__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0, int nh, float fr,
+                            float x, float y, float z, uint32_t tmask) {
+    typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
+    typedef typename std::conditional<PREC == NR_PRECISION_BF16, __bf16, _Float16>::type e16;
+    const int lane = lane_id(), g = lane >> 4;
+    const TileIn T = tile_inputs(x, y, z);
+    float a[4][8];
+    {
+        const float4 *w0 = reinterpret_cast<const float4 *>(fl) + g * 8;
+        const float *b0 = fl + 128 + g * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float4 w = w0[k];
+            const float bk = b0[k];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (!(tmask >> t & 1u)) continue;
+                float acc = w.x * T.x[t] + w.y * T.y[t] + w.z * T.z[t];
+                if (in0 == 4) acc += w.w * fr;
+                a[t][k] = fmaxf(acc + bk, 0.0f);
+            }
+        }
+    }
+    for (int jl = 0; jl < nh; ++jl) {
+        const v8 *A = reinterpret_cast<const v8 *>(lp + (size_t)jl * LP_A_ELEMS);
+        const v8 w0 = A[lane], w1 = A[64 + lane];
+        const float4 *bb = reinterpret_cast<const float4 *>(fl + 160 + 32 * jl + g * 8);
+        const float4 blo = bb[0], bhi = bb[1];
+        const f32x4 c0i = {blo.x, blo.y, blo.z, blo.w}, c1i = {bhi.x, bhi.y, bhi.z, bhi.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!(tmask >> t & 1u)) continue;
+            v8 b;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) b[e] = (e16)a[t][e];
+            f32x4 c0, c1;
+            if constexpr (PREC == NR_PRECISION_BF16) {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b, c0i, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b, c1i, 0, 0, 0);
+            } else {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b, c0i, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, b, c1i, 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                a[t][r] = fmaxf(c0[r], 0.0f);
+                a[t][4 + r] = fmaxf(c1[r], 0.0f);
+            }
+        }
+    }
+    const float *wf = fl + 160 + 32 * nh + g * 8;
+    const float bf = fl[160 + 32 * nh + 32];
+    float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (!(tmask >> t & 1u)) continue;
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(wf[k], a[t][k], acc);
+        acc += __shfl_xor(acc, 16);
+        acc += __shfl_xor(acc, 32);
+        zt[t] = acc + bf;
+    }
+    return tile_outputs(zt);
+}
+
+__device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
+                                       int prec, float fr, float x, float y, float z, uint32_t tmask) {
+    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask);
+    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask);
+    return mlp16_fp32(s32, M.in0, M.nh, fr, x, y, z, tmask);
+}
+
+__device__ __forceinline__ uint32_t tiles_of(uint64_t m) {
+    return ((m & 0xffffull) ? 1u : 0u) | (((m >> 16) & 0xffffull) ? 2u : 0u) | (((m >> 32) & 0xffffull) ? 4u : 0u) |
+           ((m >> 48) ? 8u : 0u);
+}
+
+}  // namespace nr

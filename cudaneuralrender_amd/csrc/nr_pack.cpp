@@ -125,6 +125,85 @@ bool pack_lowp(const std::vector<int> &dims, const std::vector<std::vector<float
     return true;
 }
 
+// ---- 16-point tiles (nr_mlp16.h).  Lane (j, g): point j, unit group g; register k.
+namespace {
+// fp32: unit held by (g, k): next layer MFMA -> 4k + g (ascending f32 chain over the
+// 8 k-steps x 4 lane groups); next layer final VALU -> 8g + k (chain hops 3 times).
+inline int unit16(int g, int k, bool final_consumer) { return final_consumer ? 8 * g + k : 4 * k + g; }
+// low precision: the MFMA C layout as is: register k = 4mt + r of group g = row 16mt + 4g + r
+inline int row16(int g, int k) { return 16 * (k >> 2) + 4 * g + (k & 3); }
+}  // namespace
+
+bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                  const std::vector<std::vector<float>> &B, std::vector<float> &pack) {
+    if (!fused_shape_ok(dims)) return false;
+    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    pack.assign(pk_floats(nh), 0.0f);
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) {
+            int u = unit16(g, k, nh == 0);
+            for (int i = 0; i < 4; ++i) pack[PK_L0W + (g * 8 + k) * 4 + i] = (i < in0) ? K[0][(size_t)i * 32 + u] : 0.0f;
+            pack[PK_L0B + g * 8 + k] = B[0][u];
+        }
+    for (int j = 0; j < nh; ++j) {
+        const std::vector<float> &Kj = K[j + 1];
+        bool fin = (j == nh - 1);
+        int base = PK_HID + j * PK_HID_STRIDE;
+        for (int st = 0; st < 8; ++st)
+            for (int mt = 0; mt < 2; ++mt) {
+                int m = 2 * st + mt;
+                for (int lane = 0; lane < 64; ++lane) {
+                    int i = lane & 15, kk = lane >> 4;
+                    int gp = i >> 2, rp = i & 3;
+                    int uout = fin ? 8 * gp + 4 * mt + rp : 16 * mt + 4 * rp + gp;
+                    int uin = 4 * st + kk;
+                    pack[base + ((m >> 2) * 64 + lane) * 4 + (m & 3)] = Kj[(size_t)uin * 32 + uout];
+                }
+            }
+        for (int g = 0; g < 4; ++g)
+            for (int k = 0; k < 8; ++k) pack[base + 1024 + g * 8 + k] = B[j + 1][unit16(g, k, fin)];
+    }
+    int fo = pk_final(nh);
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) pack[fo + g * 8 + k] = K[nl - 1][8 * g + k];
+    pack[fo + 32] = B[nl - 1][0];
+    return true;
+}
+
+bool pack_lowp_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                  const std::vector<std::vector<float>> &B, int precision, std::vector<uint16_t> &a_ops,
+                  std::vector<float> &fl) {
+    if (!fused_shape_ok(dims)) return false;
+    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    auto cvt = [&](float v) { return precision == NR_PRECISION_BF16 ? f2bf16(v) : f2fp16(v); };
+    a_ops.assign((size_t)nh * LP_A_ELEMS, 0);
+    fl.assign(160 + 32 * nh + 36, 0.0f);
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) {
+            int u = row16(g, k);
+            for (int i = 0; i < 4; ++i) fl[(g * 8 + k) * 4 + i] = (i < in0) ? K[0][(size_t)i * 32 + u] : 0.0f;
+            fl[128 + g * 8 + k] = B[0][u];
+        }
+    for (int j = 0; j < nh; ++j) {
+        const std::vector<float> &Kj = K[j + 1];
+        for (int mt = 0; mt < 2; ++mt)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                    int i = lane & 15, gg = lane >> 4;
+                    int uin = row16(gg, e);       // B operand element e of group gg = that unit
+                    int uout = 16 * mt + i;
+                    a_ops[(size_t)j * LP_A_ELEMS + (mt * 64 + lane) * 8 + e] = cvt(Kj[(size_t)uin * 32 + uout]);
+                }
+        for (int g = 0; g < 4; ++g)
+            for (int k = 0; k < 8; ++k) fl[160 + 32 * j + g * 8 + k] = B[j + 1][row16(g, k)];
+    }
+    int fo = 160 + 32 * nh;
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) fl[fo + g * 8 + k] = K[nl - 1][row16(g, k)];
+    fl[fo + 32] = B[nl - 1][0];
+    return true;
+}
+
 // updateViewMatrices (reference src/main.cpp:207-222), evaluated in double and
 // rounded to float once (the reference uses Eigen float arithmetic).
 void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {

@@ -1,0 +1,253 @@
+// nr_trace.hip -- persistent sphere tracer: one launch marches every ray of the frame.
+//
+// Replaces the reference's host loop (volumeRender_kernel.cu:652-689: per iteration
+// 9 GEMM launches + singleMarch + a full-image thrust scan + a blocking 4-byte D2H)
+// with a single persistent launch:
+//   * every wave owns 64 ray slots (ray state in registers, point p in lane p);
+//   * free slots are refilled from a pixel queue sharded 8 ways (one counter per
+//     shard, each on its own cache line; a wave starts on shard blockIdx % 8 and moves
+//     on when it is drained) -- the ray is generated in-lane (initMarcher :293-358);
+//   * each wave iteration runs the MLP on the live points (nr_mlp16.h, 16-point MFMA
+//     tiles, weights in LDS), then one sphere-trace step per ray (singleMarch :416-477);
+//     each ray counts its own iterations, so the reference's global iteration cap
+//     (MAX_STEPS / the configs' 64-256) holds per ray, bit for bit;
+//   * once the queue is drained the live rays are compacted into the lowest tiles, so
+//     the tail costs ceil(live/16) tiles per iteration instead of a full wave;
+//   * converged rays park {p, d} in a per-pixel slot; k_shade16 evaluates the four
+//     tetrahedral samples (surfaceNormal :361-377) and colours them (:380-413).
+#include "nr_mlp16.h"
+
+namespace nr {
+
+extern __shared__ __attribute__((aligned(16))) unsigned char nr_smem16[];
+
+struct Smem16 {
+    float *s32;       // fp32 16-wide pack
+    uint16_t *slp;    // bf16/fp16 A operands
+    float *sfl;       // float side of the low-precision pack
+};
+
+__device__ __forceinline__ Smem16 stage16(const MlpArgs &M, int prec) {
+    Smem16 S;
+    S.s32 = reinterpret_cast<float *>(nr_smem16);
+    S.slp = reinterpret_cast<uint16_t *>(nr_smem16 + M.pk_bytes);
+    S.sfl = reinterpret_cast<float *>(nr_smem16 + M.pk_bytes + M.lp_bytes);
+    const int4 *src = reinterpret_cast<const int4 *>(M.pk);
+    int4 *dst = reinterpret_cast<int4 *>(S.s32);
+    for (int i = threadIdx.x; i < M.pk_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    if (prec != NR_PRECISION_FP32) {
+        src = reinterpret_cast<const int4 *>(M.lp);
+        dst = reinterpret_cast<int4 *>(S.slp);
+        for (int i = threadIdx.x; i < M.lp_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        src = reinterpret_cast<const int4 *>(M.lpf);
+        dst = reinterpret_cast<int4 *>(S.sfl);
+        for (int i = threadIdx.x; i < M.lpf_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    return S;
+}
+
+// Ray generation for local pixel lp of the shard (initMarcher :293-358).  Returns hit.
+__device__ __forceinline__ bool gen_ray(const RenderArgs &A, long lp, F3 &p, F3 &d, float &tfar) {
+    const int lr = (int)(lp / A.W), x = (int)(lp - (long)lr * A.W);
+    const int y = ((lr / A.band) * A.nshards + A.shard) * A.band + (lr % A.band);
+    const float *M = A.inv_view;
+    F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
+               dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
+    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
+    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
+    F3 dd = normalize3(mk3(u, v, -2.0f));
+    dd = mk3(dot3(dd, mk3(M[0], M[1], M[2])), dot3(dd, mk3(M[4], M[5], M[6])), dot3(dd, mk3(M[8], M[9], M[10])));
+    F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
+    float a = dot3(dd, dd);
+    float b = (float)(2.0 * (double)dot3(Qv, dd));
+    float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
+    float disc = b * b - 4 * a * cc;
+    if (!(disc > 0)) return false;
+    float sq = sqrtf(disc);
+    float tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
+    tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
+    if (tnear < 0.0f) tnear = 0.0f;
+    p = add3(o, mul3s(dd, tnear));
+    d = dd;
+    return true;
+}
+
+template <int PREC>
+__global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+    constexpr int prec = PREC;
+    Smem16 S = stage16(M, prec);
+    const int lane = lane_id();
+    const long npix = (long)A.W * A.rows;
+    const long nchunks = (npix + 63) / 64;
+    const float fr = (float)A.frame;
+    int shard = blockIdx.x & 7, tries = 0;
+    bool qempty = false;
+    F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
+    float tfar = 0.0f;
+    uint32_t pix = 0;
+    int it = 0, maxit = 0;
+    bool live = false;
+    uint64_t nsteps = 0, nhit = 0, nconv = 0;
+    while (true) {
+        // ---- refill free slots from the pixel queue
+        if (!qempty) {
+            const uint64_t freem = __ballot(!live);
+            if (freem) {
+                const uint32_t nfree = (uint32_t)__popcll(freem);
+                uint32_t base = 0, got = 0;
+                while (true) {
+                    const long sh_chunks = shard < nchunks ? (nchunks - 1 - shard) / 8 + 1 : 0;
+                    const long total = sh_chunks * 64;
+                    uint32_t b = 0;
+                    if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
+                    base = __shfl(b, 0);
+                    if ((long)base < total) {
+                        got = (uint32_t)min((long)nfree, total - (long)base);
+                        break;
+                    }
+                    shard = (shard + 1) & 7;
+                    if (++tries >= 8) { qempty = true; break; }
+                }
+                if (got) {
+                    const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
+                    bool hit = false;
+                    if (!live && rank < got) {
+                        const uint32_t q = base + rank;
+                        const long lp = ((long)(q >> 6) * 8 + shard) * 64 + (q & 63);
+                        if (lp < npix) {
+                            T.shade_p[lp] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // not (yet) converged
+                            hit = gen_ray(A, lp, p, d, tfar);
+                            if (hit && A.max_steps > 0) {
+                                live = true;
+                                it = 0;
+                                pix = (uint32_t)lp;
+                            } else {
+                                A.out[lp] = 0u;  // background (:335-339) or no iterations at all
+                            }
+                        }
+                    }
+                    nhit += (uint64_t)__popcll(__ballot(hit));
+                }
+            }
+        }
+        uint64_t lm = __ballot(live);
+        if (!lm) {
+            if (qempty) break;
+            continue;
+        }
+        uint32_t tmask = tiles_of(lm);
+        // ---- tail: pack the live rays into the lowest tiles
+        if (qempty) {
+            const int nl = (int)__popcll(lm);
+            const int need = (nl + 15) >> 4;
+            if (__popc(tmask) > need) {
+                const int src = select_bit(lm, lane < nl ? lane : 0);
+                p = mk3(__shfl(p.x, src), __shfl(p.y, src), __shfl(p.z, src));
+                d = mk3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+                tfar = __shfl(tfar, src);
+                pix = (uint32_t)__shfl((int)pix, src);
+                it = __shfl(it, src);
+                live = lane < nl;
+                lm = __ballot(live);
+                tmask = (1u << need) - 1u;
+            }
+        }
+        // ---- MLP on every live point, then one sphere-trace step per ray
+        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr, p.x, p.y, p.z, tmask);
+        nsteps += (uint64_t)__popcll(lm);
+        bool conv = false;
+        if (live) {
+            const float ts = scene_sdf(p, sdf, A.scene, A.frame);
+            tfar -= ts;
+            if (tfar <= 0) {
+                A.out[pix] = 0u;
+                live = false;
+                maxit = max(maxit, it + 1);
+            } else {
+                p = add3(p, mul3s(d, ts));
+                if (ts < MARCHING_EPSILON) {
+                    live = false;
+                    if (it + 1 < A.max_steps) {  // coloured in the next iteration (:446-457)
+                        T.shade_p[pix] = make_float4(p.x, p.y, p.z, 1.0f);
+                        T.shade_d[pix] = make_float4(d.x, d.y, d.z, 0.0f);
+                        conv = true;
+                        maxit = max(maxit, it + 2);
+                    } else {
+                        A.out[pix] = 0u;
+                        maxit = max(maxit, it + 1);
+                    }
+                } else if (++it >= A.max_steps) {  // iteration cap: pixel stays 0 (:690)
+                    A.out[pix] = 0u;
+                    live = false;
+                    maxit = max(maxit, A.max_steps);
+                }
+            }
+        }
+        nconv += (uint64_t)__popcll(__ballot(conv));
+    }
+    // ---- frame statistics: one set of atomics per wave
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
+    if (lane == 0) {
+        if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
+        if (nhit) atomicAdd(T.stats + 1, (unsigned long long)nhit);
+        if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
+        if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
+    }
+}
+
+// Normals + colour of the converged rays: 16 rays x 4 tetrahedron samples per group.
+__global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, TraceArgs T) {
+    Smem16 S = stage16(M, NR_PRECISION_FP32);
+    const int lane = lane_id();
+    const int q = lane & 3;
+    const long npix = (long)A.W * A.rows;
+    const long nchunks = (npix + 63) / 64;
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    const float fr = (float)A.frame;
+    const F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
+    for (long c = wave; c < nchunks; c += nwaves) {
+        const long lp0 = c * 64 + lane;
+        const bool conv = lp0 < npix && T.shade_p[lp0].w != 0.0f;
+        const uint64_t m = __ballot(conv);
+        const int ncv = (int)__popcll(m);
+        for (int g0 = 0; g0 < ncv; g0 += 16) {
+            const int r = g0 + (lane >> 2);
+            const bool valid = r < ncv;
+            const long pid = c * 64 + select_bit(m, valid ? r : 0);
+            const float4 sp = T.shade_p[pid], sd = T.shade_d[pid];
+            const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
+            const int nv = min(16, ncv - g0) * 4;  // valid lanes are 0 .. nv-1
+            const uint32_t tmask = (1u << ((nv + 15) >> 4)) - 1u;
+            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr, pq.x, pq.y, pq.z, tmask);
+            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, A.frame));
+            const int l0 = lane & ~3;
+            const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
+            const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
+            const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
+            if (valid && q == 0) {
+                const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
+                A.out[pid] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
+            }
+        }
+    }
+}
+
+hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {
+    if (prec == NR_PRECISION_BF16)
+        hipLaunchKernelGGL(k_trace<NR_PRECISION_BF16>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
+    else if (prec == NR_PRECISION_FP16)
+        hipLaunchKernelGGL(k_trace<NR_PRECISION_FP16>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
+    else
+        hipLaunchKernelGGL(k_trace<NR_PRECISION_FP32>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_shade16, dim3(grid), dim3(256), smem_bytes(M, NR_PRECISION_FP32), st, A, M, T);
+    return hipGetLastError();
+}
+
+}  // namespace nr

@@ -9,7 +9,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_HOST, NR_PRECISION, NR_SCENE,
+from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_HOST, NR_PRECISION, NR_SCENE, NR_SCHEDULE,
                    NRKernelProf, NRStats, check, lib)
 
 _FP = ctypes.POINTER(ctypes.c_float)
@@ -182,6 +182,12 @@ class Renderer:
         p = NRKernelProf()
         self._chk(self._L.nr_prof_collect(self._ctx, ctypes.byref(p)))
         return p.as_dict()
+
+    def set_schedule(self, schedule):
+        """"persistent" (one k_trace launch per frame, default) or "wavefront" (one
+        k_march launch per iteration)."""
+        self._chk(self._L.nr_set_schedule(self._ctx, NR_SCHEDULE[schedule] if isinstance(schedule, str) else schedule))
+        return self
 
     def set_poll_interval(self, every):
         self._chk(self._L.nr_set_poll_interval(self._ctx, int(every)))

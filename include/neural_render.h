@@ -47,6 +47,10 @@ extern "C" {
 #define NR_COLOR_FACING 0    /* facingColor (:380-384) */
 #define NR_COLOR_MATCAP 1    /* matCapColor (:387-413) */
 
+/* march schedule (nr_set_schedule) */
+#define NR_SCHED_PERSISTENT 0 /* one persistent k_trace launch per frame (default) */
+#define NR_SCHED_WAVEFRONT 1  /* one k_march launch per iteration over a compacted ray queue */
+
 /* buffer location flags */
 #define NR_HOST 0
 #define NR_DEVICE 1
@@ -138,6 +142,7 @@ typedef struct nr_kernel_prof {
 } nr_kernel_prof;
 int nr_set_profiling(nr_ctx *ctx, int on);
 int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
+int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Host polls the live-ray count every `every` iterations to stop early (0 = never). */
 int nr_set_poll_interval(nr_ctx *ctx, int every);
 

@@ -80,10 +80,11 @@ RENDER_CASES = [
 ]
 
 
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
 @pytest.mark.parametrize("W,H,scene,color,rx,ry,zoom,steps", RENDER_CASES)
-def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, steps):
+def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, steps, schedule):
     dims, K, B = nets["plane_1"]
-    rend.load_mlp(dims, K, B).set_precision("fp32")
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_schedule(schedule)
     iv, nm = nr.camera(rx, ry, zoom)
     ct = nr.NR_COLOR_MATCAP if color == "matcap" else nr.NR_COLOR_FACING
     rend.set_view(iv, nm, 0).set_static(ct, 3).set_scene(scene).set_matcap(chrome)
@@ -94,6 +95,7 @@ def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, s
     assert not diff.any(), f"{diff.sum()} pixels differ; gpu stats {st} oracle {rst}"
     for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
         assert st[k] == rst[k], (k, st, rst)
+    rend.set_schedule("persistent")
 
 
 @pytest.mark.parametrize("geom", ["plane_2", "car_1", "plane_3", "3a3d4a90a2db90b4203936772104a82d.obj"])
@@ -159,10 +161,11 @@ def test_mlp_lowp_tolerance(rend, nets, golden, prec, tol):
     rend.set_precision("fp32")
 
 
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_render_lowp_close(rend, nets, chrome, prec):
+def test_render_lowp_close(rend, nets, chrome, prec, schedule):
     dims, K, B = nets["plane_1"]
-    rend.load_mlp(dims, K, B).set_precision(prec)
+    rend.load_mlp(dims, K, B).set_precision(prec).set_schedule(schedule)
     iv, nm = nr.camera(0, 0, 2)
     rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
     img, st = rend.render(128, 128, 128)
@@ -171,7 +174,21 @@ def test_render_lowp_close(rend, nets, chrome, prec):
     iou = (fg & fg_ref).sum() / max((fg | fg_ref).sum(), 1)
     assert iou > 0.97, iou
     assert abs(st["ray_steps"] - rst["ray_steps"]) / rst["ray_steps"] < 0.05
-    rend.set_precision("fp32")
+    rend.set_precision("fp32").set_schedule("persistent")
+
+
+def test_schedules_agree_1024(rend, nets, chrome):
+    # full benchmark frame: persistent and wavefront schedules give identical pixels/stats
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(0, 0, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    a, sa = rend.set_schedule("persistent").render(1024, 1024, 128)
+    b, sb = rend.set_schedule("wavefront").render(1024, 1024, 128)
+    rend.set_schedule("persistent")
+    assert np.array_equal(a, b)
+    for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
+        assert sa[k] == sb[k], (k, sa, sb)
 
 
 def test_render_deterministic(rend, nets, chrome):
