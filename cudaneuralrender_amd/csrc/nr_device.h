@@ -92,32 +92,48 @@ __device__ float nr_tanh(float x) {
 }
 
 __device__ __forceinline__ float smooth_union(float d1, float d2, float k) {  // :144-149
-    // h = __saturatef(0.5 + 0.5*(d2-d1)/k).  When |d2-d1| >= k the double quotient is
-    // >= 0.5 in magnitude (division and rounding are monotone, 0.5 is representable), so
-    // the saturated h is exactly 1 or 0 and the f64 division can be skipped bit-exactly.
+    // Reference: h = __saturatef(0.5 + 0.5*(d2-d1)/k); mix = d2*(1.0-h) + d1*h;
+    // return mix - k*h*(1.0-h), with the double literals promoting to f64.
+    // When |d2-d1| >= k the f64 quotient is >= 0.5 in magnitude (division and rounding
+    // are monotone, 0.5 is representable), so h is exactly 1 or 0; every remaining
+    // product is then by 0 or 1 and every sum adds a zero, all exact in f32, so the f32
+    // evaluation below is bit-identical to the f64 one (signed zeros included).
     const float t = d2 - d1;
-    float h;
-    if (t >= k) h = 1.0f;
-    else if (t <= -k) h = 0.0f;
-    else h = saturatef_((float)(0.5 + 0.5 * (double)t / (double)k));
-    float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
+    if (t >= k || t <= -k) {
+        const float h = (t >= k) ? 1.0f : 0.0f;
+        const float omh = 1.0f - h;
+        const float mix = d2 * omh + d1 * h;
+        return mix - (k * h) * omh;
+    }
+    const float h = saturatef_((float)(0.5 + 0.5 * (double)t / (double)k));
+    const float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
     return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
 }
 
 __device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
+    // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
+    // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
+    // the x values repeat in every row, so the 3 x, 3 y and 1 z coordinates are formed
+    // once with the same f64 operations and reused.
+    const float x0 = (float)((double)p.x + 0.5);
+    const float x1 = (float)((double)x0 - 0.4);
+    const float x2 = (float)((double)x1 - 0.4);
+    const float ys = (float)((double)p.y - 0.6);
+    const float y0 = (float)((double)ys + 0.4);
+    const float y1 = (float)((double)y0 + 0.4);
+    const float y2 = (float)((double)y1 + 0.4);
+    const float zc = (float)((double)p.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+    const float xx[3] = {x0 * x0, x1 * x1, x2 * x2};
+    const float yy[3] = {y0 * y0, y1 * y1, y2 * y2};
+    const float zz = zc * zc;
     float s = nsdf;
-    F3 cP = p;
-    cP.y = (float)((double)cP.y - 0.6);
-    cP.z = (float)((double)cP.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
 #pragma unroll
-    for (int i = 0; i < 9; i++) {
-        if (i % 3 == 0) {
-            cP.y = (float)((double)cP.y + 0.4);
-            cP.x = (float)((double)p.x + 0.5);
+    for (int row = 0; row < 3; ++row)
+#pragma unroll
+        for (int col = 0; col < 3; ++col) {
+            const float len = sqrtf((xx[col] + yy[row]) + zz);  // length(cP) = sqrtf(dot(cP, cP))
+            s = smooth_union(s, len - 0.1f, 0.01f);
         }
-        s = smooth_union(s, length3(cP) - 0.1f, 0.01f);
-        cP.x = (float)((double)cP.x - 0.4);
-    }
     return s;
 }
 

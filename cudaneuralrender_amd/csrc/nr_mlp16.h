@@ -18,23 +18,6 @@ namespace nr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Broadcast of the 4 tiles' inputs: lane (j, g) of tile t needs point 16t + j.
-struct TileIn {
-    float x[4], y[4], z[4];
-};
-
-__device__ __forceinline__ TileIn tile_inputs(float x, float y, float z) {
-    const int j = lane_id() & 15;
-    TileIn T;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        T.x[t] = __shfl(x, 16 * t + j);
-        T.y[t] = __shfl(y, 16 * t + j);
-        T.z[t] = __shfl(z, 16 * t + j);
-    }
-    return T;
-}
-
 // z_t lives in lane (j, 3) = 48 + j of tile t; point p = 16t + j gets it back in lane p.
 __device__ __forceinline__ float tile_outputs(const float zt[4]) {
     const int lane = lane_id(), j = lane & 15, t = lane >> 4;
@@ -43,30 +26,34 @@ __device__ __forceinline__ float tile_outputs(const float zt[4]) {
     return t == 0 ? r0 : (t == 1 ? r1 : (t == 2 ? r2 : r3));
 }
 
-__device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y, float z,
-                            uint32_t tmask) {
-    const int lane = lane_id(), g = lane >> 4;
-    const TileIn T = tile_inputs(x, y, z);
-    float a[4][8];
-    // layer 0 on VALU: fmaf chain over the inputs from +0, + bias, ReLU.  Register k of
-    // group g holds unit 4k + g (or 8g + k when the next layer is the final one).
+// FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
+template <int NT>
+__device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
+                                               float y, float z) {
+    const int lane = lane_id(), g = lane >> 4, j = lane & 15;
+    float a[NT][8];
+    f32x4 c[NT][2];
+    // layer 0 on the matrix core too: K = in0 padded to 4 (weight 0 for the pad, whose
+    // fma adds +0 to a chain that can never be -0), one v_mfma_f32_16x16x4_f32 per
+    // row tile.  Lane (j, g) feeds input g of point j.
     {
-        const float4 *w0 = reinterpret_cast<const float4 *>(s + PK_L0W) + g * 8;
-        const float *b0 = s + PK_L0B + g * 8;
+        const float w0 = s[PK_L0W + lane], w1 = s[PK_L0W + 64 + lane];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float4 w = w0[k];
-            const float bk = b0[k];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (!(tmask >> t & 1u)) continue;
-                float acc = __builtin_fmaf(w.x, T.x[t], 0.0f);
-                acc = __builtin_fmaf(w.y, T.y[t], acc);
-                acc = __builtin_fmaf(w.z, T.z[t], acc);
-                if (in0 == 4) acc = __builtin_fmaf(w.w, fr, acc);
-                a[t][k] = fmaxf(acc + bk, 0.0f);
-            }
+        for (int t = 0; t < NT; ++t) {
+            const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
+            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : (in0 == 4 ? fr : 0.0f)));
+            c[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+            c[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
         }
+        const float4 *bb = reinterpret_cast<const float4 *>(s + PK_L0B + g * 8);
+        const float4 blo = bb[0], bhi = bb[1];
+        const float bias[8] = {blo.x, blo.y, blo.z, blo.w, bhi.x, bhi.y, bhi.z, bhi.w};
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
     }
     // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
     for (int jl = 0; jl < nh; ++jl) {
@@ -74,12 +61,6 @@ __device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float 
         float4 wq[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) wq[q] = reinterpret_cast<const float4 *>(L)[q * 64 + lane];
-        f32x4 c[4][2];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            c[t][0] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            c[t][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
 #pragma unroll
         for (int st = 0; st < 8; ++st) {
 #pragma unroll
@@ -88,21 +69,20 @@ __device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float 
                 const float4 wv = wq[m >> 2];
                 const float w = (m & 3) == 0 ? wv.x : ((m & 3) == 1 ? wv.y : ((m & 3) == 2 ? wv.z : wv.w));
 #pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    if (tmask >> t & 1u) c[t][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w, a[t][st], c[t][mt], 0, 0, 0);
+                for (int t = 0; t < NT; ++t)
+                    c[t][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        w, a[t][st], st == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : c[t][mt], 0, 0, 0);
             }
         }
         const float4 *bb = reinterpret_cast<const float4 *>(L + 1024 + g * 8);
         const float4 blo = bb[0], bhi = bb[1];
         const float bias[8] = {blo.x, blo.y, blo.z, blo.w, bhi.x, bhi.y, bhi.z, bhi.w};
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (!(tmask >> t & 1u)) continue;
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
-        }
     }
     // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
     // groups 0 -> 1 -> 2 -> 3 with one cross-lane hand-off per group.
@@ -113,8 +93,7 @@ __device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float 
     for (int k = 0; k < 8; ++k) w8[k] = wf[k];
     float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        if (!(tmask >> t & 1u)) continue;
+    for (int t = 0; t < NT; ++t) {
         float acc = 0.0f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(w8[k], a[t][k], acc);
@@ -130,30 +109,40 @@ __device__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float 
     return tile_outputs(zt);
 }
 
+__device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
+                                            float z, uint32_t tmask) {
+    const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
+    if (nt >= 4) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
+    if (nt == 3) return mlp16_fp32_nt<3>(s, in0, nh, fr, x, y, z);
+    if (nt == 2) return mlp16_fp32_nt<2>(s, in0, nh, fr, x, y, z);
+    return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
+}
+
 // bf16 / fp16 hidden layers: one v_mfma_f32_16x16x32 per row tile per layer (K = 32
-// in a single instruction); layer 0 and the final layer in fp32 on VALU.  Register
-// k = 4mt + r of group g holds unit 16mt + 4g + r (the MFMA C layout, unpermuted).
-template <int PREC>
-__device__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0, int nh, float fr,
-                            float x, float y, float z, uint32_t tmask) {
+// in a single instruction, bias preloaded as the accumulator); layer 0 on the f32
+// matrix core as in the fp32 path; final layer in fp32 on VALU.  Register k = 4mt + r
+// of group g holds unit 16mt + 4g + r (the MFMA C layout, unpermuted).
+template <int PREC, int NT>
+__device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                               int nh, float fr, float x, float y, float z) {
     typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
     typedef typename std::conditional<PREC == NR_PRECISION_BF16, __bf16, _Float16>::type e16;
-    const int lane = lane_id(), g = lane >> 4;
-    const TileIn T = tile_inputs(x, y, z);
-    float a[4][8];
+    const int lane = lane_id(), g = lane >> 4, j = lane & 15;
+    float a[NT][8];
     {
-        const float4 *w0 = reinterpret_cast<const float4 *>(fl) + g * 8;
-        const float *b0 = fl + 128 + g * 8;
+        const float w0 = fl[lane], w1 = fl[64 + lane];
+        const float4 *bb = reinterpret_cast<const float4 *>(fl + 128 + g * 8);
+        const float4 blo = bb[0], bhi = bb[1];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float4 w = w0[k];
-            const float bk = b0[k];
+        for (int t = 0; t < NT; ++t) {
+            const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
+            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : (in0 == 4 ? fr : 0.0f)));
+            const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{blo.x, blo.y, blo.z, blo.w}, 0, 0, 0);
+            const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{bhi.x, bhi.y, bhi.z, bhi.w}, 0, 0, 0);
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                if (!(tmask >> t & 1u)) continue;
-                float acc = w.x * T.x[t] + w.y * T.y[t] + w.z * T.z[t];
-                if (in0 == 4) acc += w.w * fr;
-                a[t][k] = fmaxf(acc + bk, 0.0f);
+            for (int r = 0; r < 4; ++r) {
+                a[t][r] = fmaxf(c0[r], 0.0f);
+                a[t][4 + r] = fmaxf(c1[r], 0.0f);
             }
         }
     }
@@ -164,8 +153,7 @@ __device__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__rest
         const float4 blo = bb[0], bhi = bb[1];
         const f32x4 c0i = {blo.x, blo.y, blo.z, blo.w}, c1i = {bhi.x, bhi.y, bhi.z, bhi.w};
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (!(tmask >> t & 1u)) continue;
+        for (int t = 0; t < NT; ++t) {
             v8 b;
 #pragma unroll
             for (int e = 0; e < 8; ++e) b[e] = (e16)a[t][e];
@@ -188,8 +176,7 @@ __device__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__rest
     const float bf = fl[160 + 32 * nh + 32];
     float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        if (!(tmask >> t & 1u)) continue;
+    for (int t = 0; t < NT; ++t) {
         float acc = 0.0f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(wf[k], a[t][k], acc);
@@ -198,6 +185,16 @@ __device__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__rest
         zt[t] = acc + bf;
     }
     return tile_outputs(zt);
+}
+
+template <int PREC>
+__device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                            int nh, float fr, float x, float y, float z, uint32_t tmask) {
+    const int nt = 32 - __clz((int)tmask);
+    if (nt >= 4) return mlp16_lowp_nt<PREC, 4>(lp, fl, in0, nh, fr, x, y, z);
+    if (nt == 3) return mlp16_lowp_nt<PREC, 3>(lp, fl, in0, nh, fr, x, y, z);
+    if (nt == 2) return mlp16_lowp_nt<PREC, 2>(lp, fl, in0, nh, fr, x, y, z);
+    return mlp16_lowp_nt<PREC, 1>(lp, fl, in0, nh, fr, x, y, z);
 }
 
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,

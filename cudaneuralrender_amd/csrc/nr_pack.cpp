@@ -139,12 +139,15 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
     if (!fused_shape_ok(dims)) return false;
     int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
     pack.assign(pk_floats(nh), 0.0f);
-    for (int g = 0; g < 4; ++g)
-        for (int k = 0; k < 8; ++k) {
-            int u = unit16(g, k, nh == 0);
-            for (int i = 0; i < 4; ++i) pack[PK_L0W + (g * 8 + k) * 4 + i] = (i < in0) ? K[0][(size_t)i * 32 + u] : 0.0f;
-            pack[PK_L0B + g * 8 + k] = B[0][u];
+    // layer 0 as one 16x16x4 MFMA per row tile: A[row 16mt + i][k = input kk]
+    for (int mt = 0; mt < 2; ++mt)
+        for (int lane = 0; lane < 64; ++lane) {
+            int i = lane & 15, kk = lane >> 4, gp = i >> 2, rp = i & 3;
+            int uout = (nh == 0) ? 8 * gp + 4 * mt + rp : 16 * mt + 4 * rp + gp;
+            pack[PK_L0W + mt * 64 + lane] = (kk < in0) ? K[0][(size_t)kk * 32 + uout] : 0.0f;
         }
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) pack[PK_L0B + g * 8 + k] = B[0][unit16(g, k, nh == 0)];
     for (int j = 0; j < nh; ++j) {
         const std::vector<float> &Kj = K[j + 1];
         bool fin = (j == nh - 1);
@@ -178,12 +181,14 @@ bool pack_lowp_16(const std::vector<int> &dims, const std::vector<std::vector<fl
     auto cvt = [&](float v) { return precision == NR_PRECISION_BF16 ? f2bf16(v) : f2fp16(v); };
     a_ops.assign((size_t)nh * LP_A_ELEMS, 0);
     fl.assign(160 + 32 * nh + 36, 0.0f);
-    for (int g = 0; g < 4; ++g)
-        for (int k = 0; k < 8; ++k) {
-            int u = row16(g, k);
-            for (int i = 0; i < 4; ++i) fl[(g * 8 + k) * 4 + i] = (i < in0) ? K[0][(size_t)i * 32 + u] : 0.0f;
-            fl[128 + g * 8 + k] = B[0][u];
+    // layer 0: f32 16x16x4 MFMA A operand, rows in natural unit order
+    for (int mt = 0; mt < 2; ++mt)
+        for (int lane = 0; lane < 64; ++lane) {
+            int i = lane & 15, kk = lane >> 4;
+            fl[mt * 64 + lane] = (kk < in0) ? K[0][(size_t)kk * 32 + 16 * mt + i] : 0.0f;
         }
+    for (int g = 0; g < 4; ++g)
+        for (int k = 0; k < 8; ++k) fl[128 + g * 8 + k] = B[0][row16(g, k)];
     for (int j = 0; j < nh; ++j) {
         const std::vector<float> &Kj = K[j + 1];
         for (int mt = 0; mt < 2; ++mt)
