@@ -24,7 +24,8 @@ EXPORTS = [
     "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_shard_rows",
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
-    "nr_set_poll_interval", "nr_set_schedule",
+    "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
+    "nr_set_occupancy",
 ]
 
 
@@ -109,6 +110,9 @@ def lib():
         "nr_prof_collect": (I, [P, ctypes.POINTER(NRKernelProf)]),
         "nr_set_poll_interval": (I, [P, I]),
         "nr_set_schedule": (I, [P, I]),
+        "nr_set_debug": (I, [P, I]),
+        "nr_set_occupancy": (I, [P, I]),
+        "nr_debug_stamps": (I, [P, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

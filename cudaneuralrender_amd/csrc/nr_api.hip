@@ -42,6 +42,10 @@ struct nr_ctx {
     MlpArgs mlp16{};  // 16-point tiles: k_trace, k_shade16 (persistent schedule)
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
+    int debug = 0;
+    int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
+    unsigned long long *d_stamps = nullptr;
+    size_t n_stamps = 0;       // waves of the last traced launch
 
     // settings
     float inv_view[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 2};
@@ -273,7 +277,7 @@ int nr_destroy(nr_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_io); dfree(c->d_matcap);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -431,17 +435,18 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         TraceArgs T{};
         T.pix_ctr = c->d_tr;
         T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + 8 * 32);
-        T.shade_p = c->d_SP;
-        T.shade_d = c->d_SD;
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
+        int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
+        if (grid < 1) grid = 1;
+        if (c->debug & 1) {
+            if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 8));
+            T.stamps = c->d_stamps;
+            c->n_stamps = (size_t)grid * 4;
+        }
         HIPCHK(c, hipEventRecord(c->ev0, s));
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, tr_bytes, s));
-        int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * 4);
-        if (grid < 1) grid = 1;
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
         HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
-        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
-        if ((rc2 = prof_begin(c, 2, s)) != NR_OK) return rc2;
-        HIPCHK(c, launch_shade16(A, c->mlp16, T, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         if (c->profiling) c->prof_renders++;
         HIPCHK(c, hipEventRecord(c->ev1, s));
@@ -455,7 +460,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             st.iterations = (int32_t)hs[2];
             st.rays_shaded = hs[3];
             st.shade_evals = 4ull * hs[3];
-            st.launches = 3;
+            st.launches = 2;
             float ms = 0;
             HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
             st.ms_total = ms;
@@ -643,6 +648,28 @@ int nr_set_schedule(nr_ctx *c, int schedule) {
     if (schedule != NR_SCHED_PERSISTENT && schedule != NR_SCHED_WAVEFRONT)
         return set_err(c, NR_E_INVALID, "unknown schedule %d", schedule);
     c->schedule = schedule;
+    return NR_OK;
+}
+
+int nr_set_occupancy(nr_ctx *c, int blocks_per_cu) {
+    if (!c || blocks_per_cu < 0 || blocks_per_cu > 16) return set_err(c, NR_E_INVALID, "nr_set_occupancy: bad arguments");
+    c->blocks_per_cu = blocks_per_cu;
+    return NR_OK;
+}
+
+int nr_set_debug(nr_ctx *c, int flags) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    c->debug = flags;
+    return NR_OK;
+}
+
+int nr_debug_stamps(nr_ctx *c, unsigned long long *out, size_t cap, size_t *n) {
+    if (!c || !n) return set_err(c, NR_E_INVALID, "nr_debug_stamps: NULL argument");
+    *n = c->n_stamps;
+    if (!out || !c->d_stamps) return NR_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    size_t m = std::min(cap / 4, c->n_stamps);
+    HIPCHK(c, hipMemcpy(out, c->d_stamps, m * 4 * 8, hipMemcpyDeviceToHost));
     return NR_OK;
 }
 

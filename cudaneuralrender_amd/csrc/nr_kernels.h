@@ -41,8 +41,7 @@ struct QueueArgs {
 struct TraceArgs {
     uint32_t *pix_ctr;          // 8 pixel-queue shard counters, one per 128-byte line (stride 32)
     unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded
-    float4 *shade_p;            // per local pixel: converged point, w = 1 if it must be coloured
-    float4 *shade_d;            // per local pixel: ray direction
+    unsigned long long *stamps; // diagnostics (nr_set_debug): per wave {start, queue drained, end, ray-steps}
 };
 
 int smem_bytes(const MlpArgs &M, int prec);
@@ -54,7 +53,6 @@ hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &
                         hipStream_t st);
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
-hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);
 

@@ -13,11 +13,15 @@
 //     (MAX_STEPS / the configs' 64-256) holds per ray, bit for bit;
 //   * once the queue is drained the live rays are compacted into the lowest tiles, so
 //     the tail costs ceil(live/16) tiles per iteration instead of a full wave;
-//   * converged rays park {p, d} in a per-pixel slot; k_shade16 evaluates the four
-//     tetrahedral samples (surfaceNormal :361-377) and colours them (:380-413).
+//   * converged rays go to a per-wave LDS stash; whenever 16 are stashed (or the queue
+//     is drained) the wave evaluates their 4 tetrahedral samples as one full 4-tile MLP
+//     pass (surfaceNormal :361-377, always fp32) and colours them (:380-413) -- so the
+//     normal work fills the tail of the frame instead of a separate launch.
 #include "nr_mlp16.h"
 
 namespace nr {
+
+constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
 extern __shared__ __attribute__((aligned(16))) unsigned char nr_smem16[];
 
@@ -77,10 +81,15 @@ template <int PREC>
 __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     Smem16 S = stage16(M, prec);
+    __shared__ float4 stash[4][STASH][2];  // per wave: {p.xyz, pixel}, {d.xyz, -}
     const int lane = lane_id();
+    const int wid = threadIdx.x >> 6;
     const long npix = (long)A.W * A.rows;
     const long nchunks = (npix + 63) / 64;
     const float fr = (float)A.frame;
+    const int q4 = lane & 3;
+    const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
+    int nstash = 0;
     int shard = blockIdx.x & 7, tries = 0;
     bool qempty = false;
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
@@ -89,6 +98,8 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
     int it = 0, maxit = 0;
     bool live = false;
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
+    const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    unsigned long long t_start = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
         // ---- refill free slots from the pixel queue
         if (!qempty) {
@@ -107,7 +118,11 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                         break;
                     }
                     shard = (shard + 1) & 7;
-                    if (++tries >= 8) { qempty = true; break; }
+                    if (++tries >= 8) {
+                        qempty = true;
+                        if (T.stamps) t_empty = __builtin_amdgcn_s_memrealtime();
+                        break;
+                    }
                 }
                 if (got) {
                     const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
@@ -116,7 +131,6 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                         const uint32_t q = base + rank;
                         const long lp = ((long)(q >> 6) * 8 + shard) * 64 + (q & 63);
                         if (lp < npix) {
-                            T.shade_p[lp] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);  // not (yet) converged
                             hit = gen_ray(A, lp, p, d, tfar);
                             if (hit && A.max_steps > 0) {
                                 live = true;
@@ -131,9 +145,31 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                 }
             }
         }
+        // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass
+        while (nstash >= 16 || (qempty && nstash > 0)) {
+            const int nb = min(16, nstash);
+            const int k = lane >> 2;
+            const int e = nstash - nb + (k < nb ? k : 0);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const float4 sp = stash[wid][e][0], sd = stash[wid][e][1];
+            const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
+            const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
+            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr, pq.x, pq.y, pq.z, smask);
+            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, A.frame));
+            const int l0 = lane & ~3;
+            const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
+            const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
+            const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
+            if (k < nb && q4 == 0) {
+                const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
+                A.out[__float_as_uint(sp.w)] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
+            }
+            nconv += (uint64_t)nb;
+            nstash -= nb;
+        }
         uint64_t lm = __ballot(live);
         if (!lm) {
-            if (qempty) break;
+            if (qempty && nstash == 0) break;
             continue;
         }
         uint32_t tmask = tiles_of(lm);
@@ -169,8 +205,6 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                 if (ts < MARCHING_EPSILON) {
                     live = false;
                     if (it + 1 < A.max_steps) {  // coloured in the next iteration (:446-457)
-                        T.shade_p[pix] = make_float4(p.x, p.y, p.z, 1.0f);
-                        T.shade_d[pix] = make_float4(d.x, d.y, d.z, 0.0f);
                         conv = true;
                         maxit = max(maxit, it + 2);
                     } else {
@@ -184,54 +218,26 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                 }
             }
         }
-        nconv += (uint64_t)__popcll(__ballot(conv));
+        const uint64_t cm = __ballot(conv);
+        if (conv) {
+            const int slot = nstash + (int)__popcll(cm & lanemask_lt());
+            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
+            stash[wid][slot][1] = make_float4(d.x, d.y, d.z, 0.0f);
+        }
+        nstash += (int)__popcll(cm);
     }
     // ---- frame statistics: one set of atomics per wave
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
+    if (T.stamps && lane == 0) {
+        unsigned long long *st = T.stamps + 4 * gwave;
+        st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime(); st[3] = nsteps;
+    }
     if (lane == 0) {
         if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
         if (nhit) atomicAdd(T.stats + 1, (unsigned long long)nhit);
         if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
         if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
-    }
-}
-
-// Normals + colour of the converged rays: 16 rays x 4 tetrahedron samples per group.
-__global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, TraceArgs T) {
-    Smem16 S = stage16(M, NR_PRECISION_FP32);
-    const int lane = lane_id();
-    const int q = lane & 3;
-    const long npix = (long)A.W * A.rows;
-    const long nchunks = (npix + 63) / 64;
-    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-    const float fr = (float)A.frame;
-    const F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
-    for (long c = wave; c < nchunks; c += nwaves) {
-        const long lp0 = c * 64 + lane;
-        const bool conv = lp0 < npix && T.shade_p[lp0].w != 0.0f;
-        const uint64_t m = __ballot(conv);
-        const int ncv = (int)__popcll(m);
-        for (int g0 = 0; g0 < ncv; g0 += 16) {
-            const int r = g0 + (lane >> 2);
-            const bool valid = r < ncv;
-            const long pid = c * 64 + select_bit(m, valid ? r : 0);
-            const float4 sp = T.shade_p[pid], sd = T.shade_d[pid];
-            const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
-            const int nv = min(16, ncv - g0) * 4;  // valid lanes are 0 .. nv-1
-            const uint32_t tmask = (1u << ((nv + 15) >> 4)) - 1u;
-            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr, pq.x, pq.y, pq.z, tmask);
-            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, A.frame));
-            const int l0 = lane & ~3;
-            const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
-            const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
-            const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
-            if (valid && q == 0) {
-                const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                A.out[pid] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
-            }
-        }
     }
 }
 
@@ -242,11 +248,6 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
         hipLaunchKernelGGL(k_trace<NR_PRECISION_FP16>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
     else
         hipLaunchKernelGGL(k_trace<NR_PRECISION_FP32>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
-    return hipGetLastError();
-}
-
-hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(k_shade16, dim3(grid), dim3(256), smem_bytes(M, NR_PRECISION_FP32), st, A, M, T);
     return hipGetLastError();
 }
 

@@ -189,6 +189,21 @@ class Renderer:
         self._chk(self._L.nr_set_schedule(self._ctx, NR_SCHEDULE[schedule] if isinstance(schedule, str) else schedule))
         return self
 
+    def set_occupancy(self, blocks_per_cu):
+        self._chk(self._L.nr_set_occupancy(self._ctx, int(blocks_per_cu)))
+        return self
+
+    def set_debug(self, flags):
+        self._chk(self._L.nr_set_debug(self._ctx, int(flags)))
+
+    def debug_stamps(self):
+        """Per-wave {start, queue drained, end, ray-steps} of the last k_trace (100 MHz ticks)."""
+        n = ctypes.c_size_t()
+        self._chk(self._L.nr_debug_stamps(self._ctx, None, 0, ctypes.byref(n)))
+        buf = np.zeros((n.value, 4), np.uint64)
+        self._chk(self._L.nr_debug_stamps(self._ctx, buf.ctypes.data, buf.size, ctypes.byref(n)))
+        return buf
+
     def set_poll_interval(self, every):
         self._chk(self._L.nr_set_poll_interval(self._ctx, int(every)))
 

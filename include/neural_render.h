@@ -143,6 +143,13 @@ typedef struct nr_kernel_prof {
 int nr_set_profiling(nr_ctx *ctx, int on);
 int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
 int nr_set_schedule(nr_ctx *ctx, int schedule);
+/* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
+ * {start, pixel queue drained, end, ray-steps}; nr_debug_stamps copies the last
+ * frame's (4 u64 per wave, *n = waves). */
+int nr_set_debug(nr_ctx *ctx, int flags);
+/* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
+int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
+int nr_debug_stamps(nr_ctx *ctx, unsigned long long *out, size_t cap, size_t *n);
 /* Host polls the live-ray count every `every` iterations to stop early (0 = never). */
 int nr_set_poll_interval(nr_ctx *ctx, int every);
 
