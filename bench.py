@@ -13,8 +13,10 @@ re-interleaves them (nr_assemble_shards).  The frame size is fixed as N grows:
 scaling "strong".
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
-k_march, f32 MFMA bound, per-launch HIP events on the stream it runs on) and
-`cpu_baseline` (the C oracle on the host cores, N = 1 only).
+k_trace, f32 MFMA bound, per-launch HIP events on the stream it runs on) and
+`cpu_baseline` (the C oracle on the host cores, N = 1 only).  `value` is measured with
+one frame at a time; config.pipelined repeats the timing with --inflight frames in
+flight on separate streams (frame k+1's bulk fills the SIMDs frame k's tail leaves idle).
 """
 import argparse
 import json
@@ -45,6 +47,8 @@ def parse():
     ap.add_argument("--geometry", default="plane_1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight for the pipelined figure (config.pipelined); 1 = off")
     return ap.parse_args()
 
 
@@ -90,28 +94,38 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     size = a.size
-    r = nr.Renderer(local)
-    r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
-    iv, nm = nr.camera(0.0, 0.0, 2.0)
     matcap = nr.load_png(nr.matcap_path("Chrome"))
-    r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
-    stream = torch.cuda.current_stream()
-    r.set_stream(stream.cuda_stream)
+    iv, nm = nr.camera(0.0, 0.0, 2.0)
 
     rows = nr.shard_rows(size, BAND, world, rank)
     max_rows = max(nr.shard_rows(size, BAND, world, s) for s in range(world))
-    shard_buf = torch.zeros(max_rows * size, dtype=torch.int32, device="cuda")
-    gather_buf = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if rank == 0 else None
-    frame = torch.zeros(size * size, dtype=torch.int32, device="cuda") if rank == 0 else None
 
-    def step():
-        if world == 1:
-            r.render_device(frame.data_ptr(), size, size, a.max_steps)
-            return
-        r.render_shard_device(shard_buf.data_ptr(), size, size, BAND, world, rank, a.max_steps)
-        dist.gather(shard_buf, list(gather_buf.unbind(0)) if rank == 0 else None, dst=0)
-        if rank == 0:
-            r.assemble_device(gather_buf.data_ptr(), max_rows * size, frame.data_ptr(), size, size, BAND, world)
+    class Slot:
+        """One frame in flight: a renderer context on its own stream + its buffers."""
+
+        def __init__(self):
+            self.stream = torch.cuda.Stream()
+            self.r = nr.Renderer(local)
+            self.r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
+            self.r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
+            self.r.set_stream(self.stream.cuda_stream)
+            self.shard = torch.zeros(max_rows * size, dtype=torch.int32, device="cuda")
+            self.gather = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if rank == 0 else None
+            self.frame = torch.zeros(size * size, dtype=torch.int32, device="cuda") if rank == 0 else None
+
+        def step(self):
+            with torch.cuda.stream(self.stream):
+                if world == 1:
+                    self.r.render_device(self.frame.data_ptr(), size, size, a.max_steps)
+                    return
+                self.r.render_shard_device(self.shard.data_ptr(), size, size, BAND, world, rank, a.max_steps)
+                dist.gather(self.shard, list(self.gather.unbind(0)) if rank == 0 else None, dst=0)
+                if rank == 0:
+                    self.r.assemble_device(self.gather.data_ptr(), max_rows * size, self.frame.data_ptr(), size, size,
+                                           BAND, world)
+
+    slots = [Slot() for _ in range(max(1, a.inflight))]
+    r = slots[0].r
 
     # work per frame (deterministic): ray-steps of this rank's shard, summed over ranks
     st = r.render_shard(size, size, BAND, world, rank, a.max_steps)[1]
@@ -120,27 +134,41 @@ def main():
         dist.all_reduce(steps_t)
     ray_steps, shade_evals = (float(v) for v in steps_t.tolist())
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    r.prof_collect()          # drop anything recorded so far
-    r.set_profiling(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    r.set_profiling(False)
-    prof = r.prof_collect()
-    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+    def timed(nslots, profile):
+        for i in range(a.warmup):
+            slots[i % nslots].step()
+        torch.cuda.synchronize()
+        for sl in slots[:nslots]:
+            sl.r.prof_collect()          # drop anything recorded so far
+            sl.r.set_profiling(profile)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            slots[i % nslots].step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        profs = []
+        for sl in slots[:nslots]:
+            sl.r.set_profiling(False)
+            profs.append(sl.r.prof_collect())
+        dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        return float(dt_t.item()), profs
+
+    # headline: one frame at a time (each frame's launch starts after the previous one)
+    dt, profs = timed(1, True)
+    prof = profs[0]
+    # pipelined: `inflight` frames in flight on separate streams (frame k+1 fills the
+    # SIMDs that frame k's tail leaves idle)
+    dt_pipe = None
+    if a.inflight > 1:
+        dt_pipe, _ = timed(a.inflight, False)
+    frame = slots[(a.steps - 1) % (a.inflight if a.inflight > 1 else 1)].frame
 
     # parity spot-check of the timed output (outside the timed region)
     parity = None
@@ -149,10 +177,12 @@ def main():
         got = frame.cpu().numpy().view(np.uint32).reshape(size, size)
         parity = bool(np.array_equal(ref, got))
 
-    # roofline of the dominant kernel (k_march) from this rank's per-launch events
+    # roofline of the dominant kernel (k_trace) from this rank's per-launch events
     march_avg_ms = prof["march_ms"] / max(prof["march_launches"], 1)
-    local_steps = st["ray_steps"] * prof["renders"]
-    flop_per_launch = local_steps * FLOP_PER_EVAL / max(prof["march_launches"], 1)
+    # k_trace evaluates the MLP for every march step AND the 4 tetrahedral samples of
+    # every coloured ray (in-kernel shading), 14,592 algorithmic FLOP each
+    local_evals = (st["ray_steps"] + st["shade_evals"]) * prof["renders"]
+    flop_per_launch = local_evals * FLOP_PER_EVAL / max(prof["march_launches"], 1)
     achieved = flop_per_launch / (march_avg_ms * 1e-3) / 1e12 if march_avg_ms > 0 else 0.0
     peak = PEAK[a.precision]
 
@@ -182,10 +212,16 @@ def main():
             "shade_evals_per_frame": int(shade_evals),
             "parallelism": f"row-band shards x{world} + RCCL gather" if world > 1 else "single GPU",
             "parity_vs_single_gpu_render": parity,
+            "pipelined": None if dt_pipe is None else {
+                "frames_in_flight": a.inflight,
+                "value": round(ray_steps * a.steps / dt_pipe / 1e6, 3),
+                "ms_per_step": round(dt_pipe / a.steps * 1e3, 4),
+                "fps": round(a.steps / dt_pipe, 3),
+            },
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "k_march",
+            "kernel": "k_trace",
             "achieved": round(achieved, 3),
             "peak": peak,
             "unit": "TFLOP/s",
@@ -194,7 +230,8 @@ def main():
             "flop_per_launch": round(flop_per_launch, 1),
             "avg_launch_ms": round(march_avg_ms, 5),
             "launches": int(prof["march_launches"]),
-            "shade_ms_per_frame": round(prof["shade_ms"] / max(prof["renders"], 1), 4),
+            "flop_basis": "(ray-steps + shade evals) x 14,592 FLOP per launch / mean k_trace duration "
+                          "(per-launch HIP events on the context stream)",
         },
         "cpu_baseline": None,
     }

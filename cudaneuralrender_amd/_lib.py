@@ -25,7 +25,7 @@ EXPORTS = [
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
-    "nr_set_occupancy",
+    "nr_set_occupancy", "nr_set_temporal_order",
 ]
 
 
@@ -84,7 +84,7 @@ def lib():
         "nr_destroy": (I, [P]),
         "nr_last_error": (ctypes.c_char_p, [P]),
         "nr_abi_version": (I, []),
-        "nr_set_stream": (I, [P, P]),
+        "nr_set_stream": (I, [P, P, I]),
         "nr_synchronize": (I, [P]),
         "nr_load_h5": (I, [P, ctypes.c_char_p]),
         "nr_load_mlp": (I, [P, I, IP, ctypes.POINTER(FP), ctypes.POINTER(FP)]),
@@ -112,6 +112,7 @@ def lib():
         "nr_set_schedule": (I, [P, I]),
         "nr_set_debug": (I, [P, I]),
         "nr_set_occupancy": (I, [P, I]),
+        "nr_set_temporal_order": (I, [P, I]),
         "nr_debug_stamps": (I, [P, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
     }
     for name, (res, args) in sig.items():

@@ -44,6 +44,12 @@ struct nr_ctx {
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
     int debug = 0;
     int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
+    // temporal block ordering (nr_set_temporal_order)
+    int temporal = 0;
+    uint32_t *d_bcost = nullptr, *d_order[2] = {nullptr, nullptr};
+    size_t cap_blocks = 0;
+    int order_valid = 0, order_cur = 0;
+    long long order_key = -1;  // image configuration the stored order belongs to
     unsigned long long *d_stamps = nullptr;
     size_t n_stamps = 0;       // waves of the last traced launch
 
@@ -277,7 +283,7 @@ int nr_destroy(nr_ctx *c) {
     (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -287,9 +293,9 @@ int nr_destroy(nr_ctx *c) {
     return NR_OK;
 }
 
-int nr_set_stream(nr_ctx *c, void *s) {
+int nr_set_stream(nr_ctx *c, void *s, int own) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    c->stream = own ? c->own_stream : (hipStream_t)s;
     return NR_OK;
 }
 
@@ -435,6 +441,24 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         TraceArgs T{};
         T.pix_ctr = c->d_tr;
         T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + 8 * 32);
+        const int bw = (W + 7) / 8, bh = (rows + 7) / 8;
+        T.bw = bw;
+        T.nblocks = bw * bh;
+        if (c->temporal) {
+            if ((size_t)T.nblocks > c->cap_blocks) {
+                dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
+                HIPCHK(c, hipMalloc(&c->d_bcost, (size_t)T.nblocks * 4));
+                HIPCHK(c, hipMalloc(&c->d_order[0], (size_t)T.nblocks * 4));
+                HIPCHK(c, hipMalloc(&c->d_order[1], (size_t)T.nblocks * 4));
+                c->cap_blocks = T.nblocks;
+                c->order_valid = 0;
+            }
+            const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
+            if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
+            T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
+            T.bcost = c->d_bcost;
+            HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
+        }
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
@@ -448,6 +472,11 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
         HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        if (c->temporal) {  // order for the next frame of the same configuration
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, s));
+            c->order_cur ^= 1;
+            c->order_valid = 1;
+        }
         if (c->profiling) c->prof_renders++;
         HIPCHK(c, hipEventRecord(c->ev1, s));
         if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
@@ -575,7 +604,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
     }
     if (c->fused) {
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * 4);
-        HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
+        if ((c->debug & 2) == 0)
+            HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
+        else  // 32-point-tile variant (k_mlp), kept for comparison
+            HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
     } else {
         const float *a = dX;
         float *bufs[2] = {scratch, scratch + (size_t)n * maxw};
@@ -648,6 +680,13 @@ int nr_set_schedule(nr_ctx *c, int schedule) {
     if (schedule != NR_SCHED_PERSISTENT && schedule != NR_SCHED_WAVEFRONT)
         return set_err(c, NR_E_INVALID, "unknown schedule %d", schedule);
     c->schedule = schedule;
+    return NR_OK;
+}
+
+int nr_set_temporal_order(nr_ctx *c, int on) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    c->temporal = on != 0;
+    c->order_valid = 0;
     return NR_OK;
 }
 

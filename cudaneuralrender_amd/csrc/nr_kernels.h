@@ -42,6 +42,11 @@ struct TraceArgs {
     uint32_t *pix_ctr;          // 8 pixel-queue shard counters, one per 128-byte line (stride 32)
     unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded
     unsigned long long *stamps; // diagnostics (nr_set_debug): per wave {start, queue drained, end, ray-steps}
+    // pixel queue over 8x8 pixel blocks of the shard image, dispensed in `order`
+    // (NULL = raster order); bcost (may be NULL) receives each block's max ray iterations
+    const uint32_t *order;
+    uint32_t *bcost;
+    int bw, nblocks;            // blocks per row, blocks in the shard image
 };
 
 int smem_bytes(const MlpArgs &M, int prec);
@@ -53,6 +58,8 @@ hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &
                         hipStream_t st);
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
+hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
+hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);
 

@@ -30,6 +30,7 @@ __device__ __forceinline__ float tile_outputs(const float zt[4]) {
 template <int NT>
 __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
                                                float y, float z) {
+    // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
     const int lane = lane_id(), g = lane >> 4, j = lane & 15;
     float a[NT][8];
     f32x4 c[NT][2];
@@ -41,7 +42,8 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
-            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : (in0 == 4 ? fr : 0.0f)));
+            const float pw = in0 == 4 ? __shfl(fr, 16 * t + j) : 0.0f;
+            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : pw));
             c[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
             c[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
         }
@@ -136,7 +138,8 @@ __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, 
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
-            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : (in0 == 4 ? fr : 0.0f)));
+            const float pw = in0 == 4 ? __shfl(fr, 16 * t + j) : 0.0f;
+            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : pw));
             const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{blo.x, blo.y, blo.z, blo.w}, 0, 0, 0);
             const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{bhi.x, bhi.y, bhi.z, bhi.w}, 0, 0, 0);
 #pragma unroll

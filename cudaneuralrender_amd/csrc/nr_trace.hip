@@ -78,14 +78,13 @@ __device__ __forceinline__ bool gen_ray(const RenderArgs &A, long lp, F3 &p, F3 
 }
 
 template <int PREC>
-__global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     Smem16 S = stage16(M, prec);
     __shared__ float4 stash[4][STASH][2];  // per wave: {p.xyz, pixel}, {d.xyz, -}
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
-    const long npix = (long)A.W * A.rows;
-    const long nchunks = (npix + 63) / 64;
+    const long nchunks = T.nblocks;
     const float fr = (float)A.frame;
     const int q4 = lane & 3;
     const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
@@ -129,8 +128,12 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
                     bool hit = false;
                     if (!live && rank < got) {
                         const uint32_t q = base + rank;
-                        const long lp = ((long)(q >> 6) * 8 + shard) * 64 + (q & 63);
-                        if (lp < npix) {
+                        const long pos = (long)(q >> 6) * 8 + shard;
+                        const int blk = T.order ? (int)T.order[pos] : (int)pos;
+                        const int by = blk / T.bw, bx = blk - by * T.bw;
+                        const int px = bx * 8 + (q & 7), py = by * 8 + ((q >> 3) & 7);
+                        const long lp = (long)py * A.W + px;
+                        if (px < A.W && py < A.rows) {
                             hit = gen_ray(A, lp, p, d, tfar);
                             if (hit && A.max_steps > 0) {
                                 live = true;
@@ -196,25 +199,33 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
         if (live) {
             const float ts = scene_sdf(p, sdf, A.scene, A.frame);
             tfar -= ts;
+            int used = 0;  // iterations this ray consumed, if it ends now
             if (tfar <= 0) {
                 A.out[pix] = 0u;
                 live = false;
-                maxit = max(maxit, it + 1);
+                used = it + 1;
             } else {
                 p = add3(p, mul3s(d, ts));
                 if (ts < MARCHING_EPSILON) {
                     live = false;
                     if (it + 1 < A.max_steps) {  // coloured in the next iteration (:446-457)
                         conv = true;
-                        maxit = max(maxit, it + 2);
+                        used = it + 2;
                     } else {
                         A.out[pix] = 0u;
-                        maxit = max(maxit, it + 1);
+                        used = it + 1;
                     }
                 } else if (++it >= A.max_steps) {  // iteration cap: pixel stays 0 (:690)
                     A.out[pix] = 0u;
                     live = false;
-                    maxit = max(maxit, A.max_steps);
+                    used = A.max_steps;
+                }
+            }
+            if (used) {
+                maxit = max(maxit, used);
+                if (T.bcost) {
+                    const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
+                    atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
                 }
             }
         }
@@ -239,6 +250,64 @@ __global__ __launch_bounds__(256) void k_trace(RenderArgs A, MlpArgs M, TraceArg
         if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
         if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
     }
+}
+
+// Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
+// 16-point-tile path: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks.
+template <int PREC>
+__global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
+    Smem16 S = stage16(M, PREC);
+    const int lane = lane_id();
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    for (long base = wave * 64; base < n; base += nwaves * 64) {
+        const long i = base + lane;
+        const bool live = i < n;
+        float x = 0.0f, y = 0.0f, z = 0.0f, f = 0.0f;
+        if (live) {
+            const float *p = X + i * M.in0;
+            x = p[0]; y = p[1]; z = p[2];
+            if (M.in0 == 4) f = p[3];
+        }
+        const long rem = n - base;
+        const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
+        const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask);
+        if (live) Y[i] = v;
+    }
+}
+
+// Counting sort of the blocks by their cost, descending (one workgroup): the order in
+// which the next frame dispenses blocks, so that its longest rays start first.
+__global__ __launch_bounds__(1024) void k_order(const uint32_t *__restrict__ bcost, uint32_t *__restrict__ order,
+                                                int nblocks) {
+    __shared__ uint32_t hist[1024];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) atomicAdd(&hist[1023 - min(bcost[b], 1023u)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan (1024 bins, once per frame)
+        uint32_t run = 0;
+        for (int i = 0; i < 1024; ++i) { uint32_t v = hist[i]; hist[i] = run; run += v; }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x)
+        order[atomicAdd(&hist[1023 - min(bcost[b], 1023u)], 1u)] = (uint32_t)b;
+}
+
+hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, hipStream_t st) {
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, bcost, order, nblocks);
+    return hipGetLastError();
+}
+
+hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
+    const int sm = smem_bytes(M, prec);
+    if (prec == NR_PRECISION_BF16)
+        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
+    else if (prec == NR_PRECISION_FP16)
+        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
+    else
+        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP32>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {

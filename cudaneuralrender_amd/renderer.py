@@ -172,8 +172,11 @@ class Renderer:
         self._chk(self._L.nr_set_matcap(self._ctx, m.ctypes.data, m.shape[1], m.shape[0]))
         return self
 
-    def set_stream(self, stream_ptr):
-        self._chk(self._L.nr_set_stream(self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+    def set_stream(self, stream_ptr=None, own=False):
+        """Issue work on `stream_ptr` (a hipStream_t as int; 0/None = HIP's null stream,
+        e.g. torch.cuda.current_stream().cuda_stream), or on the private stream (own=True)."""
+        self._chk(self._L.nr_set_stream(self._ctx, ctypes.c_void_p(stream_ptr) if stream_ptr else None, int(own)))
+        return self
 
     def set_profiling(self, on=True):
         self._chk(self._L.nr_set_profiling(self._ctx, int(on)))
@@ -191,6 +194,10 @@ class Renderer:
 
     def set_occupancy(self, blocks_per_cu):
         self._chk(self._L.nr_set_occupancy(self._ctx, int(blocks_per_cu)))
+        return self
+
+    def set_temporal_order(self, on=True):
+        self._chk(self._L.nr_set_temporal_order(self._ctx, int(on)))
         return self
 
     def set_debug(self, flags):

@@ -73,8 +73,10 @@ int nr_destroy(nr_ctx *ctx);
 /* Last error of this context (ctx may be NULL: last error of the calling thread). */
 const char *nr_last_error(const nr_ctx *ctx);
 int nr_abi_version(void);
-/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the own stream. */
-int nr_set_stream(nr_ctx *ctx, void *hip_stream);
+/* Stream the context's work is issued on: own != 0 selects the context's private
+ * (non-blocking) stream; otherwise hip_stream is used verbatim, NULL meaning HIP's
+ * default (null) stream -- e.g. torch.cuda.current_stream().cuda_stream. */
+int nr_set_stream(nr_ctx *ctx, void *hip_stream, int own);
 int nr_synchronize(nr_ctx *ctx);
 
 /* ---- network (NeuralNetwork::load / DenseLayer ctor) ---------------------- */
@@ -147,6 +149,10 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * {start, pixel queue drained, end, ray-steps}; nr_debug_stamps copies the last
  * frame's (4 u64 per wave, *n = waves). */
 int nr_set_debug(nr_ctx *ctx, int flags);
+/* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
+ * next frame of the same size/shard dispenses blocks longest-first (pixels are
+ * unaffected -- only the order work is handed out changes). */
+int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
 int nr_debug_stamps(nr_ctx *ctx, unsigned long long *out, size_t cap, size_t *n);

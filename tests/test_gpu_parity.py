@@ -191,6 +191,22 @@ def test_schedules_agree_1024(rend, nets, chrome):
         assert sa[k] == sb[k], (k, sa, sb)
 
 
+@pytest.mark.parametrize("W,H", [(200, 131), (1024, 1024)])
+def test_temporal_order_same_pixels(rend, nets, chrome, W, H):
+    # temporal block ordering changes only the order work is handed out
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(-15, 30, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    a, sa = rend.render(W, H, 128)
+    rend.set_temporal_order(True)
+    b, sb = rend.render(W, H, 128)   # records costs, raster order
+    c, sc = rend.render(W, H, 128)   # longest-first order from the previous frame
+    rend.set_temporal_order(False)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+    assert sa["ray_steps"] == sb["ray_steps"] == sc["ray_steps"]
+
+
 def test_render_deterministic(rend, nets, chrome):
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision("fp32")
