@@ -499,3 +499,67 @@ float or_scene_sdf(float px, float py, float pz, float nsdf, int scene, int fram
 {
     return sceneSDF(mk3(px, py, pz), nsdf, scene, frame);
 }
+
+/* ------------------------------------------------------------------------
+ * The GPU kernels evaluate two pieces of the scene in a restructured but, by
+ * construction, bit-identical form (nr_device.h).  These restate those forms on
+ * the CPU so tests/test_oracle.py can check the equivalence on millions of inputs
+ * against the reference forms above.
+ */
+float or_smooth_union_ref(float d1, float d2, float k) { return sdfOpSmoothUnion(d1, d2, k); }
+
+float or_smooth_union_kernelform(float d1, float d2, float k)
+{
+    const float t = d2 - d1;
+    if (t >= k || t <= -k) {
+        const float h = (t >= k) ? 1.0f : 0.0f;
+        const float omh = 1.0f - h;
+        const float mix = d2 * omh + d1 * h;
+        return mix - (k * h) * omh;
+    }
+    const float h = saturatef((float)(0.5 + 0.5 * (double)t / (double)k));
+    const float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
+    return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
+}
+
+float or_many_sphere_kernelform(float px, float py, float pz, float nsdf, int frame)
+{
+    const float x0 = (float)((double)px + 0.5);
+    const float x1 = (float)((double)x0 - 0.4);
+    const float x2 = (float)((double)x1 - 0.4);
+    const float ys = (float)((double)py - 0.6);
+    const float y0 = (float)((double)ys + 0.4);
+    const float y1 = (float)((double)y0 + 0.4);
+    const float y2 = (float)((double)y1 + 0.4);
+    const float zc = (float)((double)pz + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+    const float xx[3] = { x0 * x0, x1 * x1, x2 * x2 };
+    const float yy[3] = { y0 * y0, y1 * y1, y2 * y2 };
+    const float zz = zc * zc;
+    float s = nsdf;
+    for (int row = 0; row < 3; ++row)
+        for (int col = 0; col < 3; ++col)
+            s = or_smooth_union_kernelform(s, sqrtf((xx[col] + yy[row]) + zz) - 0.1f, 0.01f);
+    return s;
+}
+
+float or_many_sphere_ref(float px, float py, float pz, float nsdf, int frame)
+{
+    return manySphere(mk3(px, py, pz), nsdf, frame);
+}
+
+/* Batch helpers for the equivalence tests: out[i] = f(in...). */
+void or_batch_smooth_union(const float *d1, const float *d2, long n, float k, float *ref, float *ker)
+{
+    for (long i = 0; i < n; ++i) {
+        ref[i] = or_smooth_union_ref(d1[i], d2[i], k);
+        ker[i] = or_smooth_union_kernelform(d1[i], d2[i], k);
+    }
+}
+
+void or_batch_many_sphere(const float *p, const float *nsdf, long n, int frame, float *ref, float *ker)
+{
+    for (long i = 0; i < n; ++i) {
+        ref[i] = or_many_sphere_ref(p[3 * i], p[3 * i + 1], p[3 * i + 2], nsdf[i], frame);
+        ker[i] = or_many_sphere_kernelform(p[3 * i], p[3 * i + 1], p[3 * i + 2], nsdf[i], frame);
+    }
+}

@@ -36,6 +36,10 @@ def lib():
         L.or_scene_sdf.argtypes = [ctypes.c_float] * 4 + [I, I]
         L.nr_tanh_f.restype = ctypes.c_float
         L.nr_tanh_f.argtypes = [ctypes.c_float]
+        L.or_batch_smooth_union.restype = None
+        L.or_batch_smooth_union.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
+        L.or_batch_many_sphere.restype = None
+        L.or_batch_many_sphere.argtypes = [P, P, ctypes.c_long, I, P, P]
         _lib = L
     return _lib
 
@@ -92,3 +96,22 @@ def scene_sdf(p, nsdf, scene=0, frame=0):
 
 def tanh_f(x):
     return lib().nr_tanh_f(float(x))
+
+
+def smooth_union_pair(d1, d2, k=0.01):
+    """(reference form, kernel form) of sdfOpSmoothUnion over arrays (bitwise comparable)."""
+    d1 = np.ascontiguousarray(d1, np.float32)
+    d2 = np.ascontiguousarray(d2, np.float32)
+    ref = np.zeros_like(d1)
+    ker = np.zeros_like(d1)
+    lib().or_batch_smooth_union(d1.ctypes.data, d2.ctypes.data, d1.size, k, ref.ctypes.data, ker.ctypes.data)
+    return ref, ker
+
+
+def many_sphere_pair(p, nsdf, frame=0):
+    p = np.ascontiguousarray(p, np.float32)
+    nsdf = np.ascontiguousarray(nsdf, np.float32)
+    ref = np.zeros_like(nsdf)
+    ker = np.zeros_like(nsdf)
+    lib().or_batch_many_sphere(p.ctypes.data, nsdf.ctypes.data, nsdf.size, frame, ref.ctypes.data, ker.ctypes.data)
+    return ref, ker

@@ -1,0 +1,132 @@
+"""CPU tests: the oracle against the reference's own artefacts, and the kernel-form
+restructurings against the reference forms.
+
+Golden fixtures (tests/golden/, made by make_golden.py from /root/reference):
+  weights_h5py.npz  the five .h5 files read by h5py (independent HDF5 implementation)
+  mlp_kat.npz       fp64 numpy MLP outputs (ReLU hidden, linear last layer)
+  silhouettes.npz   foreground masks of the reference renders neuralGeometries/*.h5.ppm
+"""
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+from conftest import GEOMS
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_hdf5_reader_matches_h5py(nets, golden, geom):
+    # NeuralNetwork::load (neuralNetwork.cpp:85-151): groups in HDF5 name order
+    dims, K, B = nets[geom]
+    w = golden["weights"]
+    order = [str(x) for x in w[f"{geom}/__order__"]]
+    assert order == sorted(order)
+    assert len(K) == len(order) == 9
+    assert dims == [3] + [32] * 8 + [1]
+    for i, name in enumerate(order):
+        assert np.array_equal(K[i], w[f"{geom}/{name}/kernel:0"]), name
+        assert np.array_equal(B[i], w[f"{geom}/{name}/bias:0"]), name
+    assert sum(k.size for k in K) + sum(b.size for b in B) == 7553
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_oracle_mlp_vs_fp64(nets, golden, geom):
+    dims, K, B = nets[geom]
+    X = golden["kat"]["X"]
+    y = oracle.OracleNet(K, B).forward(X)[:, 0].astype(np.float64)
+    ref = golden["kat"][geom]
+    # fp32 fmaf chains over K <= 32: |err| is a few ulp of the partial-sum magnitudes
+    assert np.abs(y - ref).max() < 5e-6
+    # the simpleInfer points (simpleInfer.cpp:81-126) are the last two rows
+    assert np.abs(y[-2:] - ref[-2:]).max() < 5e-6
+
+
+def test_oracle_batch_consistency(nets):
+    # simpleInfer batchTest (simpleInfer.cpp:112-147): identical inputs -> identical outputs
+    dims, K, B = nets["plane_1"]
+    Y = oracle.OracleNet(K, B).forward(np.zeros((50000, 3), np.float32), nthreads=4)
+    assert (Y == Y[0]).all()
+
+
+def test_oracle_lowp_close(nets, golden):
+    dims, K, B = nets["plane_1"]
+    X = golden["kat"]["X"]
+    net = oracle.OracleNet(K, B)
+    ref = golden["kat"]["plane_1"]
+    for prec, tol in [(1, 0.05), (2, 0.01)]:
+        assert np.abs(net.forward(X, precision=prec)[:, 0] - ref).max() < tol
+
+
+def _sil(golden, name):
+    s = golden["sil"]
+    shape = tuple(s[f"{name}/shape"])
+    return np.unpackbits(s[name])[: shape[0] * shape[1]].reshape(shape).astype(bool)
+
+
+@pytest.mark.parametrize("name,res,min_iou", [("plane_1", 256, 0.95), ("car_1", 128, 0.85)])
+def test_oracle_silhouette_vs_reference_render(nets, golden, name, res, min_iou):
+    """The reference's own renders (neuralGeometries/<g>.h5.ppm, 1024^2) pin coverage:
+    the pure-neural scene (sceneSDF -> tanh(nSDF), volumeRender_kernel.cu:229) at the
+    camera recovered for them.  Pixel (x, y) of a res^2 render is the
+    same ray as pixel (x*k, y*k) of the 1024^2 golden (u = x/W*2-1 has no half-pixel
+    offset), so the golden is subsampled, not resized."""
+    gold = _sil(golden, name)
+    k = gold.shape[0] // res
+    gold = gold[::k, ::k]
+    rx, ry, zoom = (float(v) for v in golden["sil"][f"{name}/camera"])
+    iv, nm = nr.camera(rx, ry, zoom)
+    dims, K, B = nets[name]
+    img, st = oracle.OracleNet(K, B).render(res, res, iv, nm, color_type=0, scene=1, max_steps=6000)
+    fg = img != 0
+    iou = (fg & gold).sum() / (fg | gold).sum()
+    assert iou >= min_iou, iou
+
+
+def test_plane2_reference_render_is_black(golden):
+    # plane_2.h5.ppm is all zeros, so it pins nothing
+    assert int(golden["sil"]["plane_2/count"]) == 0
+
+
+def test_tanh_restatement_close_to_libm():
+    xs = np.concatenate([np.linspace(-12, 12, 20001), np.geomspace(1e-12, 10, 2000), -np.geomspace(1e-12, 10, 2000)])
+    xs = xs.astype(np.float32)
+    got = np.array([oracle.tanh_f(x) for x in xs], np.float32)
+    ref = np.tanh(xs.astype(np.float64)).astype(np.float32)
+    ulps = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1
+
+
+def test_smooth_union_kernel_form_bit_exact():
+    """nr_device.h evaluates sdfOpSmoothUnion (volumeRender_kernel.cu:144-149) without the
+    f64 division when |d2-d1| >= k; bit-identical to the reference form."""
+    rng = np.random.default_rng(3)
+    n = 2_000_000
+    d1 = rng.standard_normal(n).astype(np.float32) * rng.choice([1e-4, 1e-2, 1.0], n).astype(np.float32)
+    d2 = d1 + (rng.standard_normal(n) * rng.choice([1e-3, 1e-2, 1e-1], n)).astype(np.float32)
+    k = np.float32(0.01)
+    edge = np.concatenate([d1[:1000] + k, d1[:1000] - k, np.nextafter(d1[:1000] + k, 0), np.zeros(4)]).astype(np.float32)
+    d1 = np.concatenate([d1, d1[:1000], d1[:1000], d1[:1000], [0.0, -0.0, 0.0, -0.0]]).astype(np.float32)
+    d2 = np.concatenate([d2, edge[:3000], [0.0, 0.0, -0.0, -0.0]]).astype(np.float32)
+    ref, ker = oracle.smooth_union_pair(d1, d2, 0.01)
+    assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
+
+
+@pytest.mark.parametrize("frame", [0, 7, 359])
+def test_many_sphere_kernel_form_bit_exact(frame):
+    """manySphere (volumeRender_kernel.cu:176-196) with the sphere-grid coordinates hoisted
+    out of the loop, as the kernel evaluates it."""
+    rng = np.random.default_rng(frame)
+    n = 400_000
+    p = rng.uniform(-1.3, 1.3, size=(n, 3)).astype(np.float32)
+    # concentrate some points near the sphere shells (centres x in {-0.5,-0.1,0.3}, y in
+    # {0.2,-0.2,-0.6}, z = 0.7 - frame*1.4/360) so the smooth-union slow path is taken
+    c = np.stack(np.meshgrid([-0.5, -0.1, 0.3], [-0.6, -0.2, 0.2], indexing="ij"), -1).reshape(-1, 2)
+    sel = rng.integers(0, 9, n // 2)
+    dirs = rng.standard_normal((n // 2, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    cz = 0.7 - frame * 2 * 0.7 / 360
+    centre = np.stack([c[sel, 0], c[sel, 1], np.full(n // 2, cz)], -1)
+    p[: n // 2] = (centre + dirs * (0.1 + rng.normal(0, 0.01, (n // 2, 1)))).astype(np.float32)
+    nsdf = rng.normal(0, 0.3, n).astype(np.float32)
+    ref, ker = oracle.many_sphere_pair(p, nsdf, frame)
+    assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
