@@ -718,6 +718,31 @@ int nr_set_poll_interval(nr_ctx *c, int every) {
     return NR_OK;
 }
 
+int nr_dense_forward(nr_ctx *c, const float *W, const float *b, int in, int out, int relu, const float *A, float *Z,
+                     long n, int loc) {
+    if (!c || !W || !b || in < 1 || out < 1 || n < 0 || (n > 0 && (!A || !Z)))
+        return set_err(c, NR_E_INVALID, "nr_dense_forward: bad arguments");
+    if (n == 0) return NR_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (loc == NR_DEVICE) {
+        HIPCHK(c, launch_dense(W, b, A, Z, n, in, out, relu, s));
+        return NR_OK;
+    }
+    // host buffers: stage everything
+    size_t need = (size_t)in * out + out + (size_t)n * (in + out);
+    int rc = ensure_buf(c, c->d_io, c->cap_io, need);
+    if (rc != NR_OK) return rc;
+    float *dW = c->d_io, *db = dW + (size_t)in * out, *dA = db + out, *dZ = dA + (size_t)n * in;
+    HIPCHK(c, hipMemcpyAsync(dW, W, (size_t)in * out * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(db, b, (size_t)out * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(dA, A, (size_t)n * in * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_dense(dW, db, dA, dZ, n, in, out, relu, s));
+    HIPCHK(c, hipMemcpyAsync(Z, dZ, (size_t)n * out * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return NR_OK;
+}
+
 int nr_camera(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {
     if (!inv_view || !normal) return set_err(nullptr, NR_E_INVALID, "nr_camera: NULL output");
     camera_matrices(rx, ry, zoom, tx, ty, inv_view, normal);

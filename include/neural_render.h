@@ -131,6 +131,13 @@ int nr_mlp_forward(nr_ctx *ctx, const float *X, float *Y, long n, int loc);
  * loaded network applied to A [n][dims[l]] -> Z [n][dims[l+1]]. */
 int nr_layer_forward(nr_ctx *ctx, int layer, const float *A, float *Z, long n, int loc);
 
+/* Stateless dense layer on device (or host) buffers: Z = act(W A + b) per row of A,
+ * W out-major [out][in] (DenseLayer's layout, denseLayer.cu:217-227), act = ReLU if
+ * relu != 0 else linear.  Runs on ctx's stream (DenseLayer::forward objects that are
+ * not part of a loaded network). */
+int nr_dense_forward(nr_ctx *ctx, const float *W, const float *b, int in, int out, int relu,
+                     const float *A, float *Z, long n, int loc);
+
 /* ---- measurement ------------------------------------------------------------ */
 /* Per-launch HIP events around every kernel of nr_render* on the context's stream
  * (the stream those kernels run on).  nr_prof_collect() waits for the stream, sums

@@ -1,0 +1,49 @@
+"""The headless drivers (tools/: the reference's main.cpp and simpleInfer.cpp restated
+over the C++ API of include/nr/*.hh) on the GPU, against the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "tools", "bin")
+
+
+def run(args, **kw):
+    return subprocess.run(args, capture_output=True, text=True, timeout=120, **kw)
+
+
+def test_simple_infer_batch():
+    p = run([os.path.join(BIN, "simpleInfer"), nr.geometry_path("plane_1"), "1000000"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "Woah there aren't any!!" in p.stdout
+    dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
+    y0 = oracle.OracleNet(K, B).forward(np.zeros((1, 3), np.float32))[0, 0]
+    assert f"(0.000000,0.000000,0.000000):{y0:f}" in p.stdout
+
+
+@pytest.mark.parametrize("matcap,scene", [("Chrome", "v1"), (None, "tanh")])
+def test_renderer_single_png(tmp_path, matcap, scene):
+    args = [os.path.join(BIN, "neuralSDFRenderer"), "-i", nr.geometry_path("plane_1"), "-o", str(tmp_path) + "/",
+            "-W", "96", "-H", "80", "-rx", "-20", "-ry", "30", "--single", "--max-steps", "128", "--scene", scene,
+            "--ppm"]
+    if matcap:
+        args += ["-M", nr.matcap_path(matcap)]
+    p = run(args)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "volumeRender, Throughput =" in p.stdout
+    png = nr.load_png(str(tmp_path / "plane_1.h5.png"))
+    dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
+    iv, nm = nr.camera(-20, 30, 2.0)
+    mc = nr.load_png(nr.matcap_path(matcap)) if matcap else None
+    ref, _ = oracle.OracleNet(K, B).render(96, 80, iv, nm, color_type=1 if matcap else 0,
+                                           scene=0 if scene == "v1" else 1, matcap=mc, max_steps=128)
+    # savePNG reverses the byte stream: the saved image is the frame rotated 180 degrees
+    assert np.array_equal(png, ref[::-1, ::-1])
+    ppm = open(str(tmp_path / "plane_1.h5.png.ppm"), "rb").read()
+    assert ppm.startswith(b"P6\n96\n80\n255\n")
