@@ -186,6 +186,17 @@ def main():
     achieved = flop_per_launch / (march_avg_ms * 1e-3) / 1e12 if march_avg_ms > 0 else 0.0
     peak = PEAK[a.precision]
 
+    # HBM traffic of k_trace from the PMC pass committed under profiles/ (rocprofv3 --pmc
+    # FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 2x fetch correction) when it was
+    # collected on this workload; bench.py cannot read PMC counters itself
+    traffic = None
+    try:
+        tp = json.load(open(os.path.join(REPO, "profiles", "r1_pmc_traffic.json")))
+        if a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1:
+            traffic = tp["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        traffic = None
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -226,7 +237,8 @@ def main():
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (profiles/r1_pmc_traffic.json)",
             "flop_per_launch": round(flop_per_launch, 1),
             "avg_launch_ms": round(march_avg_ms, 5),
             "launches": int(prof["march_launches"]),
