@@ -603,7 +603,8 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         dX = hx;
     }
     if (c->fused) {
-        int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * 4);
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 4;
+        int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if ((c->debug & 2) == 0)
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
         else  // 32-point-tile variant (k_mlp), kept for comparison
