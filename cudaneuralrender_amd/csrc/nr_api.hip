@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +47,9 @@ struct nr_ctx {
     int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
     // temporal block ordering (nr_set_temporal_order)
     int temporal = 0;
+    // age hold (nr_set_age_hold)
+    int hold_age = 0, hold_prio = 2;
+    int spread = 16;  // nr_set_pixel_spread (16: measured 2-3% faster than block-major on configs[1])
     uint32_t *d_bcost = nullptr, *d_order[2] = {nullptr, nullptr};
     size_t cap_blocks = 0;
     int order_valid = 0, order_cur = 0;
@@ -444,6 +448,10 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         const int bw = (W + 7) / 8, bh = (rows + 7) / 8;
         T.bw = bw;
         T.nblocks = bw * bh;
+        T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
+        T.hold_prio = c->hold_prio;
+        T.itmap = (c->debug & 8) != 0;
+        T.spread = c->spread;
         if (c->temporal) {
             if ((size_t)T.nblocks > c->cap_blocks) {
                 dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
@@ -688,6 +696,19 @@ int nr_set_temporal_order(nr_ctx *c, int on) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
     c->temporal = on != 0;
     c->order_valid = 0;
+    return NR_OK;
+}
+
+int nr_set_age_hold(nr_ctx *c, int age, int prio) {
+    if (!c || age < 0 || prio < 0 || prio > 3) return set_err(c, NR_E_INVALID, "nr_set_age_hold: bad arguments");
+    c->hold_age = age;
+    c->hold_prio = prio;
+    return NR_OK;
+}
+
+int nr_set_pixel_spread(nr_ctx *c, int group_blocks) {
+    if (!c || group_blocks < 0 || group_blocks > 65536) return set_err(c, NR_E_INVALID, "nr_set_pixel_spread: bad arguments");
+    c->spread = group_blocks;
     return NR_OK;
 }
 

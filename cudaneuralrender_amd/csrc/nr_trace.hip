@@ -77,6 +77,16 @@ __device__ __forceinline__ bool gen_ray(const RenderArgs &A, long lp, F3 &p, F3 
     return true;
 }
 
+// s_setprio takes an immediate
+__device__ __forceinline__ void set_priority(int prio) {
+    switch (prio) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
 template <int PREC>
 __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
@@ -91,6 +101,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     int nstash = 0;
     int shard = blockIdx.x & 7, tries = 0;
     bool qempty = false;
+    bool hold = false;  // age hold (TraceArgs::hold_age): no refill, packed tiles, raised priority
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
     float tfar = 0.0f;
     uint32_t pix = 0;
@@ -101,7 +112,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     unsigned long long t_start = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
         // ---- refill free slots from the pixel queue
-        if (!qempty) {
+        if (!qempty && !hold) {
             const uint64_t freem = __ballot(!live);
             if (freem) {
                 const uint32_t nfree = (uint32_t)__popcll(freem);
@@ -128,10 +139,19 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                     bool hit = false;
                     if (!live && rank < got) {
                         const uint32_t q = base + rank;
-                        const long pos = (long)(q >> 6) * 8 + shard;
+                        uint32_t bq = q >> 6, pq = q & 63;
+                        if (T.spread > 1) {
+                            const uint32_t G = (uint32_t)T.spread;
+                            const uint32_t sh_chunks = (uint32_t)((nchunks - 1 - shard) / 8 + 1);
+                            const uint32_t g = q / (64u * G), r = q - g * 64u * G;
+                            const uint32_t nbg = min(G, sh_chunks - g * G);
+                            pq = r / nbg;
+                            bq = g * G + (r - pq * nbg);
+                        }
+                        const long pos = (long)bq * 8 + shard;
                         const int blk = T.order ? (int)T.order[pos] : (int)pos;
                         const int by = blk / T.bw, bx = blk - by * T.bw;
-                        const int px = bx * 8 + (q & 7), py = by * 8 + ((q >> 3) & 7);
+                        const int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
                         const long lp = (long)py * A.W + px;
                         if (px < A.W && py < A.rows) {
                             hit = gen_ray(A, lp, p, d, tfar);
@@ -163,7 +183,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
             const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
             const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
-            if (k < nb && q4 == 0) {
+            if (k < nb && q4 == 0 && !T.itmap) {
                 const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
                 A.out[__float_as_uint(sp.w)] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
             }
@@ -176,8 +196,8 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             continue;
         }
         uint32_t tmask = tiles_of(lm);
-        // ---- tail: pack the live rays into the lowest tiles
-        if (qempty) {
+        // ---- tail / age hold: pack the live rays into the lowest tiles
+        if (qempty || hold) {
             const int nl = (int)__popcll(lm);
             const int need = (nl + 15) >> 4;
             if (__popc(tmask) > need) {
@@ -223,6 +243,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             }
             if (used) {
                 maxit = max(maxit, used);
+                if (T.itmap) A.out[pix] = (uint32_t)used;
                 if (T.bcost) {
                     const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
                     atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
@@ -236,6 +257,11 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             stash[wid][slot][1] = make_float4(d.x, d.y, d.z, 0.0f);
         }
         nstash += (int)__popcll(cm);
+        const bool h = __ballot(live && it >= T.hold_age) != 0;
+        if (h != hold) {
+            hold = h;
+            set_priority(h ? T.hold_prio : 0);
+        }
     }
     // ---- frame statistics: one set of atomics per wave
 #pragma unroll

@@ -154,7 +154,8 @@ int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
 int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
  * {start, pixel queue drained, end, ray-steps}; nr_debug_stamps copies the last
- * frame's (4 u64 per wave, *n = waves). */
+ * frame's (4 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
+ * schedule writes each hit pixel's iteration count instead of its colour. */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are
@@ -162,6 +163,17 @@ int nr_set_debug(nr_ctx *ctx, int flags);
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
+/* Age hold (persistent schedule): a wave holding a ray that has marched `age` or more
+ * iterations stops taking new pixels, packs its live rays into the fewest 16-ray tiles
+ * and raises its issue priority to `prio` (0-3) until they finish, so long rays march
+ * at a short per-iteration latency while the other waves keep the matrix cores busy
+ * (age 0 = off).  Pixels are unaffected. */
+int nr_set_age_hold(nr_ctx *ctx, int age, int prio);
+/* Pixel spread (persistent schedule): the pixel queue deals each group of
+ * `group_blocks` 8x8 blocks pixel-major -- one refill takes one pixel from each of up
+ * to 64 blocks -- so the rays of one slow block are spread over many waves (default 16;
+ * 0 = block-major).  Pixels are unaffected. */
+int nr_set_pixel_spread(nr_ctx *ctx, int group_blocks);
 int nr_debug_stamps(nr_ctx *ctx, unsigned long long *out, size_t cap, size_t *n);
 /* Host polls the live-ray count every `every` iterations to stop early (0 = never). */
 int nr_set_poll_interval(nr_ctx *ctx, int every);

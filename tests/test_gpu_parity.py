@@ -215,3 +215,42 @@ def test_render_deterministic(rend, nets, chrome):
     a, sa = rend.render(1024, 1024, 128)
     b, sb = rend.render(1024, 1024, 128)
     assert np.array_equal(a, b) and sa["ray_steps"] == sb["ray_steps"]
+
+
+@pytest.mark.parametrize("W,H", [(200, 131), (1024, 1024)])
+def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
+    # pixel spread, age hold (with issue priority) and occupancy only change which wave
+    # marches which ray and when: pixels and statistics are identical
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(-15, 30, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    ref, sref = rend.set_pixel_spread(0).render(W, H, 128)
+    try:
+        for spread, age, prio, bpc in [(16, 0, 0, 0), (64, 0, 0, 3), (1000, 0, 0, 1), (16, 32, 2, 3), (0, 8, 3, 2)]:
+            rend.set_pixel_spread(spread).set_age_hold(age, prio).set_occupancy(bpc)
+            img, st = rend.render(W, H, 128)
+            assert np.array_equal(img, ref), (spread, age, prio, bpc)
+            for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
+                assert st[k] == sref[k], (k, spread, age, prio, bpc)
+    finally:
+        rend.set_pixel_spread(16).set_age_hold(0, 2).set_occupancy(0)
+
+
+def test_iteration_map(rend, nets, chrome):
+    # debug bit 3: each pixel holds the iterations its ray used (a converged ray counts
+    # the colouring iteration too), so the map sums to ray-steps + shaded rays
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    iv, nm = nr.camera(0, 0, 2)
+    rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    img, st = rend.render(256, 256, 128)
+    rend.set_debug(8)
+    try:
+        m, st2 = rend.render(256, 256, 128)
+    finally:
+        rend.set_debug(0)
+    assert st2["ray_steps"] == st["ray_steps"]
+    assert int(m.astype(np.int64).sum()) == st["ray_steps"] + st["rays_shaded"]
+    assert m.max() == st["iterations"] <= 128
+    assert ((m > 0) | (img == 0)).all()
