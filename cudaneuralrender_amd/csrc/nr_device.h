@@ -131,8 +131,17 @@ __device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
     for (int row = 0; row < 3; ++row)
 #pragma unroll
         for (int col = 0; col < 3; ++col) {
-            const float len = sqrtf((xx[col] + yy[row]) + zz);  // length(cP) = sqrtf(dot(cP, cP))
-            s = smooth_union(s, len - 0.1f, 0.01f);
+            // Far sphere: if |cP| > s + 0.1111 with s + 0.1111 < 1000, d2 = |cP| - 0.1
+            // exceeds s by more than k = 0.01 plus every rounding error of |cP|, d2 and
+            // d2 - s (each < 1e-4 at these magnitudes), so smooth_union takes h = 1 and
+            // returns (d2 * 0 + s) - 0 = s + 0 (d2 > 0 whenever s is a zero; finite sq
+            // keeps d2 * 0 from being NaN) -- decided without the correctly rounded sqrt.
+            const float sq = (xx[col] + yy[row]) + zz;
+            const float T = s + 0.1111f;
+            if (T > 0.0f && T < 1000.0f && sq > T * T && sq < 1e30f)
+                s = s + 0.0f;
+            else
+                s = smooth_union(s, sqrtf(sq) - 0.1f, 0.01f);  // length(cP) = sqrtf(dot(cP, cP))
         }
     return s;
 }

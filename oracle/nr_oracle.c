@@ -538,7 +538,14 @@ float or_many_sphere_kernelform(float px, float py, float pz, float nsdf, int fr
     float s = nsdf;
     for (int row = 0; row < 3; ++row)
         for (int col = 0; col < 3; ++col)
-            s = or_smooth_union_kernelform(s, sqrtf((xx[col] + yy[row]) + zz) - 0.1f, 0.01f);
+        {
+            const float sq = (xx[col] + yy[row]) + zz;
+            const float T = s + 0.1111f;
+            if (T > 0.0f && T < 1000.0f && sq > T * T && sq < 1e30f)   /* sphere farther than s + k: the union returns s */
+                s = s + 0.0f;
+            else
+                s = or_smooth_union_kernelform(s, sqrtf(sq) - 0.1f, 0.01f);
+        }
     return s;
 }
 

@@ -130,3 +130,25 @@ def test_many_sphere_kernel_form_bit_exact(frame):
     nsdf = rng.normal(0, 0.3, n).astype(np.float32)
     ref, ker = oracle.many_sphere_pair(p, nsdf, frame)
     assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
+
+
+@pytest.mark.parametrize("frame", [0, 17])
+def test_many_sphere_far_test_bit_exact(frame):
+    """The kernel decides 'sphere farther than s + k' from |cP|^2 without the sqrt
+    (nr_device.h many_sphere); points placed on shells of radius s + 0.1111 (+- tiny to
+    +- 1e-3) around the 9 sphere centres probe that threshold."""
+    rng = np.random.default_rng(5 + frame)
+    n = 1_000_000
+    c = np.stack(np.meshgrid([-0.5, -0.1, 0.3], [-0.6, -0.2, 0.2], indexing="ij"), -1).reshape(-1, 2)
+    cz = 0.7 - frame * 2 * 0.7 / 360
+    sel = rng.integers(0, 9, n)
+    dirs = rng.standard_normal((n, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    s = np.concatenate([rng.normal(0, 0.3, n // 2), rng.uniform(-0.2, 3, n - n // 2)]).astype(np.float32)
+    s[:8] = [0.0, -0.0, -0.1111, -0.2, 999.0, 1e4, np.inf, np.nan]
+    rad = np.abs(s.astype(np.float64) + 0.1111 + rng.normal(0, 1e-6, n) * rng.choice([0, 1, 1e2, 1e3], n))
+    rad = np.nan_to_num(rad, nan=0.5, posinf=0.5)
+    centre = np.stack([c[sel, 0], c[sel, 1], np.full(n, cz)], -1)
+    p = (centre + dirs * rad[:, None]).astype(np.float32)
+    ref, ker = oracle.many_sphere_pair(p, s, frame)
+    assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
