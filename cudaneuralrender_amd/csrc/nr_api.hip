@@ -451,7 +451,9 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
         T.hold_prio = c->hold_prio;
         T.itmap = (c->debug & 8) != 0;
-        T.spread = c->spread;
+        T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
+        T.inv_bw = 1.0 / (double)T.bw;
+        T.inv_band = 1.0 / (double)band;
         if (c->temporal) {
             if ((size_t)T.nblocks > c->cap_blocks) {
                 dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
@@ -707,7 +709,8 @@ int nr_set_age_hold(nr_ctx *c, int age, int prio) {
 }
 
 int nr_set_pixel_spread(nr_ctx *c, int group_blocks) {
-    if (!c || group_blocks < 0 || group_blocks > 65536) return set_err(c, NR_E_INVALID, "nr_set_pixel_spread: bad arguments");
+    if (!c || group_blocks < 0 || group_blocks > 65536 || (group_blocks & (group_blocks - 1)))
+        return set_err(c, NR_E_INVALID, "nr_set_pixel_spread: group_blocks must be 0 or a power of two <= 65536");
     c->spread = group_blocks;
     return NR_OK;
 }

@@ -50,11 +50,12 @@ struct TraceArgs {
     // age hold: a wave holding a ray of >= hold_age iterations stops refilling, packs
     // its rays into the lowest tiles and issues at priority hold_prio (INT_MAX = off)
     int hold_age, hold_prio;
-    // pixel spread: the queue deals a group of `spread` blocks pixel-major (a refill
+    // pixel spread: the queue deals a group of 2^spread_shift blocks pixel-major (a refill
     // takes one pixel from each of 64 blocks), so a block of long rays is marched by 64
     // different waves instead of one (0/1 = block-major)
-    int spread;
-    int itmap;                  // diagnostics: write each pixel's iteration count instead of its colour
+    int spread_shift;           // log2 of the spread group (0 = block-major)
+    int itmap;
+    double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r                  // diagnostics: write each pixel's iteration count instead of its colour
 };
 
 int smem_bytes(const MlpArgs &M, int prec);

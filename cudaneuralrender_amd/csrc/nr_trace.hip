@@ -51,10 +51,25 @@ __device__ __forceinline__ Smem16 stage16(const MlpArgs &M, int prec) {
     return S;
 }
 
-// Ray generation for local pixel lp of the shard (initMarcher :293-358).  Returns hit.
-__device__ __forceinline__ bool gen_ray(const RenderArgs &A, long lp, F3 &p, F3 &d, float &tfar) {
-    const int lr = (int)(lp / A.W), x = (int)(lp - (long)lr * A.W);
-    const int y = ((lr / A.band) * A.nshards + A.shard) * A.band + (lr % A.band);
+// n / d (d >= 1) from a precomputed f64 reciprocal: n * (1/d) = (n/d)(1 + e), |e| <= 2^-52,
+// is within n/d * 2^-52 < 1/d of n/d -- closer than any non-integer n/d is to an
+// integer -- so the truncation is the quotient or, for an exact multiple, one less,
+// which the remainder test repairs.
+__device__ __forceinline__ uint32_t udiv_r(uint32_t n, uint32_t d, double inv_d) {
+    uint32_t q = (uint32_t)((double)n * inv_d);
+    if (n - q * d >= d) ++q;
+    return q;
+}
+
+// Ray generation for pixel x of local row lr of the shard (initMarcher :293-358).
+// Returns hit.
+__device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T, int x, int lr, F3 &p, F3 &d,
+                                        float &tfar) {
+    int y = lr;
+    if (A.nshards > 1) {
+        const int bi = (int)udiv_r((uint32_t)lr, (uint32_t)A.band, T.inv_band);
+        y = (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
+    }
     const float *M = A.inv_view;
     F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
                dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
@@ -140,21 +155,22 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                     if (!live && rank < got) {
                         const uint32_t q = base + rank;
                         uint32_t bq = q >> 6, pq = q & 63;
-                        if (T.spread > 1) {
-                            const uint32_t G = (uint32_t)T.spread;
+                        if (T.spread_shift) {
+                            const int sh = T.spread_shift;
+                            const uint32_t G = 1u << sh;
                             const uint32_t sh_chunks = (uint32_t)((nchunks - 1 - shard) / 8 + 1);
-                            const uint32_t g = q / (64u * G), r = q - g * 64u * G;
+                            const uint32_t g = q >> (6 + sh), r = q & ((64u << sh) - 1u);
                             const uint32_t nbg = min(G, sh_chunks - g * G);
-                            pq = r / nbg;
+                            pq = nbg == G ? r >> sh : r / nbg;  // a short group only at the end
                             bq = g * G + (r - pq * nbg);
                         }
                         const long pos = (long)bq * 8 + shard;
                         const int blk = T.order ? (int)T.order[pos] : (int)pos;
-                        const int by = blk / T.bw, bx = blk - by * T.bw;
+                        const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
                         const int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
                         const long lp = (long)py * A.W + px;
                         if (px < A.W && py < A.rows) {
-                            hit = gen_ray(A, lp, p, d, tfar);
+                            hit = gen_ray(A, T, px, py, p, d, tfar);
                             if (hit && A.max_steps > 0) {
                                 live = true;
                                 it = 0;

@@ -225,9 +225,11 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
     rend.load_mlp(dims, K, B).set_precision("fp32")
     iv, nm = nr.camera(-15, 30, 2)
     rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    with pytest.raises(nr.NRError):
+        rend.set_pixel_spread(3)   # groups are powers of two
     ref, sref = rend.set_pixel_spread(0).render(W, H, 128)
     try:
-        for spread, age, prio, bpc in [(16, 0, 0, 0), (64, 0, 0, 3), (1000, 0, 0, 1), (16, 32, 2, 3), (0, 8, 3, 2)]:
+        for spread, age, prio, bpc in [(16, 0, 0, 0), (64, 0, 0, 3), (1024, 0, 0, 1), (1, 0, 0, 0), (16, 32, 2, 3), (0, 8, 3, 2)]:
             rend.set_pixel_spread(spread).set_age_hold(age, prio).set_occupancy(bpc)
             img, st = rend.render(W, H, 128)
             assert np.array_equal(img, ref), (spread, age, prio, bpc)
