@@ -50,6 +50,7 @@ struct nr_ctx {
     // age hold (nr_set_age_hold)
     int hold_age = 0, hold_prio = 2;
     int spread = 16;  // nr_set_pixel_spread (16: measured 2-3% faster than block-major on configs[1])
+    int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
     uint32_t *d_bcost = nullptr, *d_order[2] = {nullptr, nullptr};
     size_t cap_blocks = 0;
     int order_valid = 0, order_cur = 0;
@@ -440,8 +441,9 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     int rc2;
     if (c->schedule == NR_SCHED_PERSISTENT) {
         // 8 shard counters on their own 128-byte lines, then 4 x u64 stats
+        // (a second set for the cost probe)
         const size_t tr_bytes = 8 * 128 + 4 * 8;
-        if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, tr_bytes));
+        if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
         TraceArgs T{};
         T.pix_ctr = c->d_tr;
         T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + 8 * 32);
@@ -449,12 +451,16 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.bw = bw;
         T.nblocks = bw * bh;
         T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
-        T.hold_prio = c->hold_prio;
+        T.hold_prio = c->hold_prio & 3;
+        T.hold_refill = c->hold_prio >= 4;
         T.itmap = (c->debug & 8) != 0;
         T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
         T.inv_bw = 1.0 / (double)T.bw;
         T.inv_band = 1.0 / (double)band;
-        if (c->temporal) {
+        const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
+        if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
+        const bool probe = c->probe_steps > 0 && max_steps > 0 && !(c->temporal && c->order_valid);
+        if (c->temporal || probe) {
             if ((size_t)T.nblocks > c->cap_blocks) {
                 dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
                 HIPCHK(c, hipMalloc(&c->d_bcost, (size_t)T.nblocks * 4));
@@ -463,11 +469,10 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
                 c->cap_blocks = T.nblocks;
                 c->order_valid = 0;
             }
-            const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
-            if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
+        }
+        if (c->temporal) {
             T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
             T.bcost = c->d_bcost;
-            HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
         }
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
@@ -478,12 +483,37 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             c->n_stamps = (size_t)grid * 4;
         }
         HIPCHK(c, hipEventRecord(c->ev0, s));
-        HIPCHK(c, hipMemsetAsync(c->d_tr, 0, tr_bytes, s));
+        HIPCHK(c, hipMemsetAsync(c->d_tr, 0, (probe ? 2 : 1) * tr_bytes, s));
+        if (probe) {
+            // cost probe: march each block's centre ray for at most probe_steps iterations,
+            // then hand the blocks out longest-first
+            if ((rc2 = prof_begin(c, 0, s)) != NR_OK) return rc2;
+            HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
+            TraceArgs P = T;
+            P.probe = 1;
+            P.take = c->probe_take;
+            P.pix_ctr = c->d_tr + tr_bytes / 4;
+            P.stats = reinterpret_cast<unsigned long long *>(c->d_tr + tr_bytes / 4 + 8 * 32);
+            P.stamps = nullptr;
+            P.order = nullptr;
+            P.bcost = c->d_bcost;
+            P.spread_shift = 0;
+            P.hold_age = INT_MAX;
+            RenderArgs Ap = A;
+            Ap.max_steps = std::min(max_steps, c->probe_steps);
+            const long pwaves = ((long)T.nblocks + P.take - 1) / P.take;
+            const int pgrid = (int)std::max<long>(1, std::min<long>((pwaves + 3) / 4, grid));
+            HIPCHK(c, launch_trace(Ap, c->mlp16, P, c->precision, pgrid, s));
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur], T.nblocks, T.bw, c->probe_dilate, s));
+            if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+            T.order = c->d_order[c->order_cur];
+        }
+        if (T.bcost) HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
         HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         if (c->temporal) {  // order for the next frame of the same configuration
-            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, s));
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, 0, s));
             c->order_cur ^= 1;
             c->order_valid = 1;
         }
@@ -702,7 +732,7 @@ int nr_set_temporal_order(nr_ctx *c, int on) {
 }
 
 int nr_set_age_hold(nr_ctx *c, int age, int prio) {
-    if (!c || age < 0 || prio < 0 || prio > 3) return set_err(c, NR_E_INVALID, "nr_set_age_hold: bad arguments");
+    if (!c || age < 0 || prio < 0 || prio > 7) return set_err(c, NR_E_INVALID, "nr_set_age_hold: bad arguments");
     c->hold_age = age;
     c->hold_prio = prio;
     return NR_OK;
@@ -712,6 +742,15 @@ int nr_set_pixel_spread(nr_ctx *c, int group_blocks) {
     if (!c || group_blocks < 0 || group_blocks > 65536 || (group_blocks & (group_blocks - 1)))
         return set_err(c, NR_E_INVALID, "nr_set_pixel_spread: group_blocks must be 0 or a power of two <= 65536");
     c->spread = group_blocks;
+    return NR_OK;
+}
+
+int nr_set_cost_probe(nr_ctx *c, int max_steps, int rays_per_wave) {
+    if (!c || max_steps < 0 || max_steps > 1023 || rays_per_wave < 1 || rays_per_wave > 64)
+        return set_err(c, NR_E_INVALID, "nr_set_cost_probe: bad arguments");
+    c->probe_steps = max_steps;
+    c->probe_take = rays_per_wave;
+    c->probe_dilate = (c->debug & 16) ? 0 : 1;
     return NR_OK;
 }
 

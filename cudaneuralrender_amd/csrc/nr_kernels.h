@@ -49,13 +49,15 @@ struct TraceArgs {
     int bw, nblocks;            // blocks per row, blocks in the shard image
     // age hold: a wave holding a ray of >= hold_age iterations stops refilling, packs
     // its rays into the lowest tiles and issues at priority hold_prio (INT_MAX = off)
-    int hold_age, hold_prio;
+    int hold_age, hold_prio, hold_refill;  // hold_refill: priority only, keep refilling
     // pixel spread: the queue deals a group of 2^spread_shift blocks pixel-major (a refill
     // takes one pixel from each of 64 blocks), so a block of long rays is marched by 64
     // different waves instead of one (0/1 = block-major)
     int spread_shift;           // log2 of the spread group (0 = block-major)
     int itmap;
-    double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r                  // diagnostics: write each pixel's iteration count instead of its colour
+    double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r
+    // cost probe (k_trace<.., true>): one ray per block, at most `take` per wave refill
+    int probe, take;                  // diagnostics: write each pixel's iteration count instead of its colour
 };
 
 int smem_bytes(const MlpArgs &M, int prec);
@@ -68,7 +70,7 @@ hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
-hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, hipStream_t st);
+hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int bw, int dilate, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);
 

@@ -102,7 +102,10 @@ __device__ __forceinline__ void set_priority(int prio) {
     }
 }
 
-template <int PREC>
+// PROBE: the cost-probe pre-pass (TraceArgs::probe) -- one ray per 8x8 block, at most
+// T.take rays per wave, no pixels written; each block's bcost gets its probe ray's
+// iteration count (max_steps is the probe's cap).
+template <int PREC, bool PROBE>
 __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     Smem16 S = stage16(M, prec);
@@ -127,14 +130,15 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     unsigned long long t_start = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
         // ---- refill free slots from the pixel queue
-        if (!qempty && !hold) {
+        if (!qempty && !(hold && !T.hold_refill)) {
             const uint64_t freem = __ballot(!live);
             if (freem) {
-                const uint32_t nfree = (uint32_t)__popcll(freem);
+                const uint32_t nfree = PROBE ? min((uint32_t)__popcll(freem), (uint32_t)T.take)
+                                             : (uint32_t)__popcll(freem);
                 uint32_t base = 0, got = 0;
                 while (true) {
                     const long sh_chunks = shard < nchunks ? (nchunks - 1 - shard) / 8 + 1 : 0;
-                    const long total = sh_chunks * 64;
+                    const long total = PROBE ? sh_chunks : sh_chunks * 64;
                     uint32_t b = 0;
                     if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
                     base = __shfl(b, 0);
@@ -155,7 +159,10 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                     if (!live && rank < got) {
                         const uint32_t q = base + rank;
                         uint32_t bq = q >> 6, pq = q & 63;
-                        if (T.spread_shift) {
+                        if (PROBE) {
+                            bq = q;
+                            pq = 4 * 8 + 4;  // the block's centre pixel
+                        } else if (T.spread_shift) {
                             const int sh = T.spread_shift;
                             const uint32_t G = 1u << sh;
                             const uint32_t sh_chunks = (uint32_t)((nchunks - 1 - shard) / 8 + 1);
@@ -167,7 +174,11 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                         const long pos = (long)bq * 8 + shard;
                         const int blk = T.order ? (int)T.order[pos] : (int)pos;
                         const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
-                        const int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
+                        int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
+                        if (PROBE) {
+                            px = min(px, A.W - 1);
+                            py = min(py, A.rows - 1);
+                        }
                         const long lp = (long)py * A.W + px;
                         if (px < A.W && py < A.rows) {
                             hit = gen_ray(A, T, px, py, p, d, tfar);
@@ -175,7 +186,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                                 live = true;
                                 it = 0;
                                 pix = (uint32_t)lp;
-                            } else {
+                            } else if (!PROBE) {
                                 A.out[lp] = 0u;  // background (:335-339) or no iterations at all
                             }
                         }
@@ -184,8 +195,12 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                 }
             }
         }
-        // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass
-        while (nstash >= 16 || (qempty && nstash > 0)) {
+        // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass.
+        // Once the queue is drained a partial pass waits until the wave's last ray has
+        // ended: a pass costs a full MLP latency on the tail's critical path whatever
+        // its size, and the marching rays must not wait for it.
+        uint64_t lm = __ballot(live);
+        while (nstash >= 16 || (qempty && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
@@ -206,14 +221,13 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             nconv += (uint64_t)nb;
             nstash -= nb;
         }
-        uint64_t lm = __ballot(live);
         if (!lm) {
             if (qempty && nstash == 0) break;
             continue;
         }
         uint32_t tmask = tiles_of(lm);
         // ---- tail / age hold: pack the live rays into the lowest tiles
-        if (qempty || hold) {
+        if (qempty || (hold && !T.hold_refill)) {
             const int nl = (int)__popcll(lm);
             const int need = (nl + 15) >> 4;
             if (__popc(tmask) > need) {
@@ -237,7 +251,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
             if (tfar <= 0) {
-                A.out[pix] = 0u;
+                if (!PROBE) A.out[pix] = 0u;
                 live = false;
                 used = it + 1;
             } else {
@@ -245,21 +259,21 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                 if (ts < MARCHING_EPSILON) {
                     live = false;
                     if (it + 1 < A.max_steps) {  // coloured in the next iteration (:446-457)
-                        conv = true;
+                        conv = !PROBE;
                         used = it + 2;
                     } else {
-                        A.out[pix] = 0u;
+                        if (!PROBE) A.out[pix] = 0u;
                         used = it + 1;
                     }
                 } else if (++it >= A.max_steps) {  // iteration cap: pixel stays 0 (:690)
-                    A.out[pix] = 0u;
+                    if (!PROBE) A.out[pix] = 0u;
                     live = false;
                     used = A.max_steps;
                 }
             }
             if (used) {
                 maxit = max(maxit, used);
-                if (T.itmap) A.out[pix] = (uint32_t)used;
+                if (!PROBE && T.itmap) A.out[pix] = (uint32_t)used;
                 if (T.bcost) {
                     const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
                     atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
@@ -319,13 +333,29 @@ __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__rest
 }
 
 // Counting sort of the blocks by their cost, descending (one workgroup): the order in
-// which the next frame dispenses blocks, so that its longest rays start first.
+// which the next frame dispenses blocks, so that its longest rays start first.  With
+// `dilate`, a block's key is the max over its 3x3 neighbourhood (bw blocks per row) --
+// for a probe that saw one ray per block, a long ray next door marks a likely edge.
+__device__ __forceinline__ uint32_t order_key(const uint32_t *__restrict__ bcost, int b, int nblocks, int bw,
+                                              int dilate) {
+    uint32_t v = bcost[b];
+    if (dilate) {
+        const int by = b / bw, bx = b - by * bw, bh = (nblocks + bw - 1) / bw;
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int x = bx + dx, y = by + dy;
+                if (x >= 0 && x < bw && y >= 0 && y < bh && y * bw + x < nblocks) v = max(v, bcost[y * bw + x]);
+            }
+    }
+    return 1023 - min(v, 1023u);
+}
+
 __global__ __launch_bounds__(1024) void k_order(const uint32_t *__restrict__ bcost, uint32_t *__restrict__ order,
-                                                int nblocks) {
+                                                int nblocks, int bw, int dilate) {
     __shared__ uint32_t hist[1024];
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) atomicAdd(&hist[1023 - min(bcost[b], 1023u)], 1u);
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) atomicAdd(&hist[order_key(bcost, b, nblocks, bw, dilate)], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {  // exclusive scan (1024 bins, once per frame)
         uint32_t run = 0;
@@ -333,11 +363,11 @@ __global__ __launch_bounds__(1024) void k_order(const uint32_t *__restrict__ bco
     }
     __syncthreads();
     for (int b = threadIdx.x; b < nblocks; b += blockDim.x)
-        order[atomicAdd(&hist[1023 - min(bcost[b], 1023u)], 1u)] = (uint32_t)b;
+        order[atomicAdd(&hist[order_key(bcost, b, nblocks, bw, dilate)], 1u)] = (uint32_t)b;
 }
 
-hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, hipStream_t st) {
-    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, bcost, order, nblocks);
+hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int bw, int dilate, hipStream_t st) {
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, st, bcost, order, nblocks, bw, dilate);
     return hipGetLastError();
 }
 
@@ -353,12 +383,22 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
 }
 
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {
-    if (prec == NR_PRECISION_BF16)
-        hipLaunchKernelGGL(k_trace<NR_PRECISION_BF16>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
-    else if (prec == NR_PRECISION_FP16)
-        hipLaunchKernelGGL(k_trace<NR_PRECISION_FP16>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
-    else
-        hipLaunchKernelGGL(k_trace<NR_PRECISION_FP32>, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, T);
+    const int sm = smem_bytes(M, prec);
+    if (T.probe) {
+        if (prec == NR_PRECISION_BF16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+    } else {
+        if (prec == NR_PRECISION_BF16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false>), dim3(grid), dim3(256), sm, st, A, M, T);
+    }
     return hipGetLastError();
 }
 

@@ -208,6 +208,12 @@ class Renderer:
         self._chk(self._L.nr_set_pixel_spread(self._ctx, int(group_blocks)))
         return self
 
+    def set_cost_probe(self, max_steps, rays_per_wave=16):
+        """Persistent schedule: probe each 8x8 block's centre ray (capped at max_steps
+        iterations) before the frame and dispense blocks longest-first (0 = off)."""
+        self._chk(self._L.nr_set_cost_probe(self._ctx, int(max_steps), int(rays_per_wave)))
+        return self
+
     def set_temporal_order(self, on=True):
         self._chk(self._L.nr_set_temporal_order(self._ctx, int(on)))
         return self

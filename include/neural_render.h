@@ -174,6 +174,12 @@ int nr_set_age_hold(nr_ctx *ctx, int age, int prio);
  * to 64 blocks -- so the rays of one slow block are spread over many waves (default 16;
  * 0 = block-major).  Pixels are unaffected. */
 int nr_set_pixel_spread(nr_ctx *ctx, int group_blocks);
+/* Cost probe (persistent schedule): before each frame, march the centre ray of every
+ * 8x8 block for at most `max_steps` iterations (`rays_per_wave` rays per wave, so the
+ * probe runs at short per-iteration latency), then hand the blocks out in decreasing
+ * order of their probe's iteration count, so the frame's longest rays start first
+ * (max_steps 0 = off; a valid temporal order takes precedence).  Pixels are unaffected. */
+int nr_set_cost_probe(nr_ctx *ctx, int max_steps, int rays_per_wave);
 int nr_debug_stamps(nr_ctx *ctx, unsigned long long *out, size_t cap, size_t *n);
 /* Host polls the live-ray count every `every` iterations to stop early (0 = never). */
 int nr_set_poll_interval(nr_ctx *ctx, int every);

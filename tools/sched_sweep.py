@@ -1,6 +1,6 @@
 """Scheduling sweep of the persistent tracer on the bench workload.  Runs on the GPU box.
 
-    python tools/sched_sweep.py --grid "bpc,age,prio,temporal[,spread];..."
+    python tools/sched_sweep.py --grid "bpc,age,prio,temporal[,spread[,probe_steps[,probe_take]]]];..."
 For each schedule: frame time (median and min over --frames renders, HIP events around
 the k_trace launch) and a bit-exactness check against the first schedule's image --
 scheduling changes only the order work is handed out, never a pixel."""
@@ -26,11 +26,12 @@ matcap = nr.load_png(nr.matcap_path("Chrome"))
 ref = None
 out = torch.zeros(a.size * a.size, dtype=torch.int32, device="cuda")
 for spec in a.grid.split(";"):
-    v = [int(x) for x in spec.split(",")] + [0]
-    bpc, age, prio, temporal, spread = v[:5]
+    v = [int(x) for x in spec.split(",")] + [16, 0, 16][len(spec.split(",")) - 4:]
+    bpc, age, prio, temporal, spread, pst, ptake = v[:7]
     r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
     r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
     r.set_occupancy(bpc).set_age_hold(age, prio).set_temporal_order(temporal).set_pixel_spread(spread)
+    r.set_cost_probe(pst, ptake)
     for _ in range(3):
         r.render_device(out.data_ptr(), a.size, a.size, a.steps)
     ms = []
@@ -42,7 +43,7 @@ for spec in a.grid.split(";"):
         ref = img
     same = bool(np.array_equal(img, ref))
     ms = np.array(ms)
-    print(f"bpc {bpc} hold age {age:3d} prio {prio} temporal {temporal} spread {spread:3d}: "
+    print(f"bpc {bpc} hold {age:3d}/{prio} temporal {temporal} spread {spread:3d} probe {pst:3d}/{ptake:2d}: "
           f"median {np.median(ms):.3f} ms  min {ms.min():.3f} ms  "
           f"Mray-steps/s {(st['ray_steps'] + st['shade_evals']) / np.median(ms) / 1e3:.0f}  identical {same}",
           flush=True)
