@@ -20,6 +20,8 @@
 #include <vector>
 
 #include "nr_internal.h"
+
+constexpr int NR_MAX_QUEUES = 64;
 #include "nr_kernels.h"
 
 using namespace nr;
@@ -27,6 +29,8 @@ using namespace nr;
 struct nr_ctx {
     int device = 0;
     hipStream_t own_stream = nullptr, stream = nullptr;
+    bool use_own = true;  // stream = own_stream, created lazily: a context driven on a
+                          // caller's stream never takes a hardware queue of its own
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string err;
 
@@ -51,6 +55,8 @@ struct nr_ctx {
     int hold_age = 0, hold_prio = 2;
     int spread = 16;  // nr_set_pixel_spread (16: measured 2-3% faster than block-major on configs[1])
     int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
+    int wave_rays = 64;  // nr_set_wave_rays
+    int nq_shift = 3;    // nr_set_queue_shards: 8
     uint32_t *d_bcost = nullptr, *d_order[2] = {nullptr, nullptr};
     size_t cap_blocks = 0;
     int order_valid = 0, order_cur = 0;
@@ -262,6 +268,25 @@ int nr_abi_version(void) { return NR_ABI_VERSION; }
 
 const char *nr_last_error(const nr_ctx *ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
+// The context's stream: the caller's (nr_set_stream) or the private one, created here on
+// first use.  Returns NULL only if that creation failed (error recorded).
+#define GET_STREAM(c, s)                                           \
+    hipStream_t s = cur_stream(c);                                 \
+    if ((c)->use_own && !(c)->own_stream) return NR_E_HIP;
+
+static hipStream_t cur_stream(nr_ctx *c) {
+    if (c->use_own && !c->own_stream) {
+        if (hipSetDevice(c->device) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+            c->own_stream = nullptr;
+            set_err(c, NR_E_HIP, "stream creation failed");
+            return nullptr;
+        }
+        c->stream = c->own_stream;
+    }
+    return c->stream;
+}
+
 int nr_create(int device, nr_ctx **out) {
     if (!out) return set_err(nullptr, NR_E_INVALID, "nr_create: out is NULL");
     *out = nullptr;
@@ -272,12 +297,12 @@ int nr_create(int device, nr_ctx **out) {
     nr_ctx *c = new (std::nothrow) nr_ctx();
     if (!c) return set_err(nullptr, NR_E_NOMEM, "out of host memory");
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipEventCreate(&c->ev0) != hipSuccess ||
+        hipEventCreate(&c->ev1) != hipSuccess) {
         delete c;
         return set_err(nullptr, NR_E_HIP, "stream/event creation failed");
     }
-    c->stream = c->own_stream;
+    c->use_own = true;  // the private stream is created on first use (cur_stream)
     *out = c;
     return NR_OK;
 }
@@ -285,7 +310,7 @@ int nr_create(int device, nr_ctx **out) {
 int nr_destroy(nr_ctx *c) {
     if (!c) return NR_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (!(c->use_own && !c->own_stream)) (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
     dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
@@ -300,13 +325,17 @@ int nr_destroy(nr_ctx *c) {
 
 int nr_set_stream(nr_ctx *c, void *s, int own) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    c->use_own = own != 0;
     c->stream = own ? c->own_stream : (hipStream_t)s;
     return NR_OK;
 }
 
 int nr_synchronize(nr_ctx *c) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    {
+        GET_STREAM(c, s_);
+        HIPCHK(c, hipStreamSynchronize(s_));
+    }
     return NR_OK;
 }
 
@@ -436,17 +465,18 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
     memcpy(A.inv_view, c->inv_view, sizeof A.inv_view);
     memcpy(A.normal, c->normal, sizeof A.normal);
-    hipStream_t s = c->stream;
+    GET_STREAM(c, s);
     int cus = num_cus(c->device);
     int rc2;
     if (c->schedule == NR_SCHED_PERSISTENT) {
         // 8 shard counters on their own 128-byte lines, then 4 x u64 stats
         // (a second set for the cost probe)
-        const size_t tr_bytes = 8 * 128 + 4 * 8;
+        const size_t tr_bytes = NR_MAX_QUEUES * 128 + 4 * 8;
         if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
         TraceArgs T{};
         T.pix_ctr = c->d_tr;
-        T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + 8 * 32);
+        T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + NR_MAX_QUEUES * 32);
+        T.nq_shift = c->nq_shift;
         const int bw = (W + 7) / 8, bh = (rows + 7) / 8;
         T.bw = bw;
         T.nblocks = bw * bh;
@@ -457,6 +487,8 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
         T.inv_bw = 1.0 / (double)T.bw;
         T.inv_band = 1.0 / (double)band;
+        T.take = c->wave_rays;
+        T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
         const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
         if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
         const bool probe = c->probe_steps > 0 && max_steps > 0 && !(c->temporal && c->order_valid);
@@ -478,7 +510,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         if (c->debug & 1) {
-            if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 8));
+            if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 8 * 8));
             T.stamps = c->d_stamps;
             c->n_stamps = (size_t)grid * 4;
         }
@@ -492,8 +524,9 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             TraceArgs P = T;
             P.probe = 1;
             P.take = c->probe_take;
+            P.lane_cap = P.take >= 64 ? ~0ull : (1ull << P.take) - 1ull;
             P.pix_ctr = c->d_tr + tr_bytes / 4;
-            P.stats = reinterpret_cast<unsigned long long *>(c->d_tr + tr_bytes / 4 + 8 * 32);
+            P.stats = reinterpret_cast<unsigned long long *>(c->d_tr + tr_bytes / 4 + NR_MAX_QUEUES * 32);
             P.stamps = nullptr;
             P.order = nullptr;
             P.bcost = c->d_bcost;
@@ -612,7 +645,8 @@ int nr_assemble_shards(nr_ctx *c, const uint32_t *src, size_t stride, uint32_t *
     if (loc == NR_DEVICE) {
         if (!c) return set_err(nullptr, NR_E_INVALID, "device assembly needs a context");
         HIPCHK(c, hipSetDevice(c->device));
-        HIPCHK(c, launch_assemble(src, stride, dst, W, H, band, nshards, c->stream));
+        GET_STREAM(c, s);
+        HIPCHK(c, launch_assemble(src, stride, dst, W, H, band, nshards, s));
         return NR_OK;
     }
     for (int y = 0; y < H; ++y) {
@@ -628,7 +662,7 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
     if (n == 0) return NR_OK;
     HIPCHK(c, hipSetDevice(c->device));
     int nl = (int)c->dims.size() - 1, in0 = c->dims[0], outn = c->dims[nl];
-    hipStream_t s = c->stream;
+    GET_STREAM(c, s);
     const float *dX = X;
     float *dY = Y;
     int rc;
@@ -645,7 +679,9 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
     if (c->fused) {
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 4;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
-        if ((c->debug & 2) == 0)
+        if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
+            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, s));
+        else if ((c->debug & 2) == 0)
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
         else  // 32-point-tile variant (k_mlp), kept for comparison
             HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
@@ -672,7 +708,7 @@ int nr_layer_forward(nr_ctx *c, int layer, const float *A, float *Z, long n, int
     if (n == 0) return NR_OK;
     HIPCHK(c, hipSetDevice(c->device));
     int in = c->dims[layer], out = c->dims[layer + 1];
-    hipStream_t s = c->stream;
+    GET_STREAM(c, s);
     const float *dA = A;
     float *dZ = Z;
     if (loc != NR_DEVICE) {
@@ -700,7 +736,10 @@ int nr_set_profiling(nr_ctx *c, int on) {
 int nr_prof_collect(nr_ctx *c, nr_kernel_prof *out) {
     if (!c || !out) return set_err(c, NR_E_INVALID, "nr_prof_collect: NULL argument");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    {
+        GET_STREAM(c, s_);
+        HIPCHK(c, hipStreamSynchronize(s_));
+    }
     nr_kernel_prof p{};
     for (auto &r : c->recs) {
         float ms = 0;
@@ -754,6 +793,19 @@ int nr_set_cost_probe(nr_ctx *c, int max_steps, int rays_per_wave) {
     return NR_OK;
 }
 
+int nr_set_queue_shards(nr_ctx *c, int n) {
+    if (!c || n < 1 || n > NR_MAX_QUEUES || (n & (n - 1)))
+        return set_err(c, NR_E_INVALID, "nr_set_queue_shards: n must be a power of two in [1, %d]", NR_MAX_QUEUES);
+    c->nq_shift = 31 - __builtin_clz((unsigned)n);
+    return NR_OK;
+}
+
+int nr_set_wave_rays(nr_ctx *c, int rays) {
+    if (!c || rays < 1 || rays > 64) return set_err(c, NR_E_INVALID, "nr_set_wave_rays: rays must be in [1, 64]");
+    c->wave_rays = rays;
+    return NR_OK;
+}
+
 int nr_set_occupancy(nr_ctx *c, int blocks_per_cu) {
     if (!c || blocks_per_cu < 0 || blocks_per_cu > 16) return set_err(c, NR_E_INVALID, "nr_set_occupancy: bad arguments");
     c->blocks_per_cu = blocks_per_cu;
@@ -770,9 +822,12 @@ int nr_debug_stamps(nr_ctx *c, unsigned long long *out, size_t cap, size_t *n) {
     if (!c || !n) return set_err(c, NR_E_INVALID, "nr_debug_stamps: NULL argument");
     *n = c->n_stamps;
     if (!out || !c->d_stamps) return NR_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    size_t m = std::min(cap / 4, c->n_stamps);
-    HIPCHK(c, hipMemcpy(out, c->d_stamps, m * 4 * 8, hipMemcpyDeviceToHost));
+    {
+        GET_STREAM(c, s_);
+        HIPCHK(c, hipStreamSynchronize(s_));
+    }
+    size_t m = std::min(cap / 8, c->n_stamps);
+    HIPCHK(c, hipMemcpy(out, c->d_stamps, m * 8 * 8, hipMemcpyDeviceToHost));
     return NR_OK;
 }
 
@@ -788,7 +843,7 @@ int nr_dense_forward(nr_ctx *c, const float *W, const float *b, int in, int out,
         return set_err(c, NR_E_INVALID, "nr_dense_forward: bad arguments");
     if (n == 0) return NR_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    GET_STREAM(c, s);
     if (loc == NR_DEVICE) {
         HIPCHK(c, launch_dense(W, b, A, Z, n, in, out, relu, s));
         return NR_OK;

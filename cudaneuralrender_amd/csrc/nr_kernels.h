@@ -39,7 +39,8 @@ struct QueueArgs {
 
 // Persistent-schedule state (nr_trace.hip).
 struct TraceArgs {
-    uint32_t *pix_ctr;          // 8 pixel-queue shard counters, one per 128-byte line (stride 32)
+    uint32_t *pix_ctr;          // 2^nq_shift pixel-queue shard counters, one per 128-byte line (stride 32)
+    int nq_shift;
     unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded
     unsigned long long *stamps; // diagnostics (nr_set_debug): per wave {start, queue drained, end, ray-steps}
     // pixel queue over 8x8 pixel blocks of the shard image, dispensed in `order`
@@ -56,8 +57,9 @@ struct TraceArgs {
     int spread_shift;           // log2 of the spread group (0 = block-major)
     int itmap;
     double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r
-    // cost probe (k_trace<.., true>): one ray per block, at most `take` per wave refill
-    int probe, take;                  // diagnostics: write each pixel's iteration count instead of its colour
+    // cost probe (k_trace<.., true>): one ray per block
+    int probe, take;
+    uint64_t lane_cap;          // lanes a wave may fill: (1 << take) - 1, all 64 for take = 64                  // diagnostics: write each pixel's iteration count instead of its colour
 };
 
 int smem_bytes(const MlpArgs &M, int prec);
@@ -70,6 +72,7 @@ hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
+hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st);
 hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int bw, int dilate, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);

@@ -117,7 +117,8 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     const int q4 = lane & 3;
     const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
     int nstash = 0;
-    int shard = blockIdx.x & 7, tries = 0;
+    const int nq = 1 << T.nq_shift;  // pixel-queue shards
+    int shard = blockIdx.x & (nq - 1), tries = 0;
     bool qempty = false;
     bool hold = false;  // age hold (TraceArgs::hold_age): no refill, packed tiles, raised priority
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
@@ -126,18 +127,23 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     int it = 0, maxit = 0;
     bool live = false;
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
+    uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
+    unsigned long long ph[4] = {0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene+step
+    const bool timing = T.stamps != nullptr;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     unsigned long long t_start = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
+        if (timing) tph = __builtin_amdgcn_s_memtime();
         // ---- refill free slots from the pixel queue
         if (!qempty && !(hold && !T.hold_refill)) {
-            const uint64_t freem = __ballot(!live);
+            // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
+            // 2 tiles per iteration (short iterations when a frame shard is small)
+            const uint64_t freem = __ballot(!live) & T.lane_cap;
             if (freem) {
-                const uint32_t nfree = PROBE ? min((uint32_t)__popcll(freem), (uint32_t)T.take)
-                                             : (uint32_t)__popcll(freem);
+                const uint32_t nfree = (uint32_t)__popcll(freem);
                 uint32_t base = 0, got = 0;
                 while (true) {
-                    const long sh_chunks = shard < nchunks ? (nchunks - 1 - shard) / 8 + 1 : 0;
+                    const long sh_chunks = shard < nchunks ? ((nchunks - 1 - shard) >> T.nq_shift) + 1 : 0;
                     const long total = PROBE ? sh_chunks : sh_chunks * 64;
                     uint32_t b = 0;
                     if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
@@ -146,8 +152,8 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                         got = (uint32_t)min((long)nfree, total - (long)base);
                         break;
                     }
-                    shard = (shard + 1) & 7;
-                    if (++tries >= 8) {
+                    shard = (shard + 1) & (nq - 1);
+                    if (++tries >= nq) {
                         qempty = true;
                         if (T.stamps) t_empty = __builtin_amdgcn_s_memrealtime();
                         break;
@@ -165,13 +171,13 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                         } else if (T.spread_shift) {
                             const int sh = T.spread_shift;
                             const uint32_t G = 1u << sh;
-                            const uint32_t sh_chunks = (uint32_t)((nchunks - 1 - shard) / 8 + 1);
+                            const uint32_t sh_chunks = (uint32_t)(((nchunks - 1 - shard) >> T.nq_shift) + 1);
                             const uint32_t g = q >> (6 + sh), r = q & ((64u << sh) - 1u);
                             const uint32_t nbg = min(G, sh_chunks - g * G);
                             pq = nbg == G ? r >> sh : r / nbg;  // a short group only at the end
                             bq = g * G + (r - pq * nbg);
                         }
-                        const long pos = (long)bq * 8 + shard;
+                        const long pos = ((long)bq << T.nq_shift) + shard;
                         const int blk = T.order ? (int)T.order[pos] : (int)pos;
                         const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
                         int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
@@ -199,6 +205,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         // Once the queue is drained a partial pass waits until the wave's last ray has
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
         // its size, and the marching rays must not wait for it.
+        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
         uint64_t lm = __ballot(live);
         while (nstash >= 16 || (qempty && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
@@ -221,6 +228,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             nconv += (uint64_t)nb;
             nstash -= nb;
         }
+        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; tph = t; }
         if (!lm) {
             if (qempty && nstash == 0) break;
             continue;
@@ -244,7 +252,14 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr, p.x, p.y, p.z, tmask);
+        if (timing) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            ph[2] += t - tph; tph = t;
+        }
         nsteps += (uint64_t)__popcll(lm);
+        ++wit;
+        wit_tail += qempty ? 1u : 0u;
         bool conv = false;
         if (live) {
             const float ts = scene_sdf(p, sdf, A.scene, A.frame);
@@ -287,6 +302,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             stash[wid][slot][1] = make_float4(d.x, d.y, d.z, 0.0f);
         }
         nstash += (int)__popcll(cm);
+        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[3] += t - tph; tph = t; }
         const bool h = __ballot(live && it >= T.hold_age) != 0;
         if (h != hold) {
             hold = h;
@@ -297,8 +313,10 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
     if (T.stamps && lane == 0) {
-        unsigned long long *st = T.stamps + 4 * gwave;
-        st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime(); st[3] = nsteps;
+        unsigned long long *st = T.stamps + 8 * gwave;
+        st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime();
+        st[3] = ((unsigned long long)wit_tail << 32) | wit;
+        st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
     }
     if (lane == 0) {
         if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
@@ -330,6 +348,35 @@ __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__rest
         const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask);
         if (live) Y[i] = v;
     }
+}
+
+// Diagnostic (nr_set_debug bit 6): latency of the fp32 MLP on NT tiles for one wave
+// alone on its SIMD -- `reps` back-to-back evaluations, each input depending on the
+// previous output.  Y[0] = shader cycles per evaluation, Y[1..64] = the last outputs.
+template <int NT>
+__global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
+                                                    int reps) {
+    Smem16 S = stage16(M, NR_PRECISION_FP32);
+    const int lane = lane_id();
+    float x = X[3 * lane], y = X[3 * lane + 1], z = X[3 * lane + 2], v = 0.0f;
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < reps; ++r) {
+        v = mlp16_fp32_nt<NT>(S.s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
+    Y[1 + lane] = v;
+}
+
+hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st) {
+    const int sm = smem_bytes(M, NR_PRECISION_FP32);
+    if (nt <= 1) hipLaunchKernelGGL(k_mlp_latency<1>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 2) hipLaunchKernelGGL(k_mlp_latency<2>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 3) hipLaunchKernelGGL(k_mlp_latency<3>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else hipLaunchKernelGGL(k_mlp_latency<4>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    return hipGetLastError();
 }
 
 // Counting sort of the blocks by their cost, descending (one workgroup): the order in

@@ -214,6 +214,16 @@ class Renderer:
         self._chk(self._L.nr_set_cost_probe(self._ctx, int(max_steps), int(rays_per_wave)))
         return self
 
+    def set_wave_rays(self, rays):
+        """Persistent schedule: at most `rays` (1-64) rays per wave at once."""
+        self._chk(self._L.nr_set_wave_rays(self._ctx, int(rays)))
+        return self
+
+    def set_queue_shards(self, n):
+        """Persistent schedule: number of pixel-queue counters (power of two <= 64)."""
+        self._chk(self._L.nr_set_queue_shards(self._ctx, int(n)))
+        return self
+
     def set_temporal_order(self, on=True):
         self._chk(self._L.nr_set_temporal_order(self._ctx, int(on)))
         return self
@@ -222,10 +232,12 @@ class Renderer:
         self._chk(self._L.nr_set_debug(self._ctx, int(flags)))
 
     def debug_stamps(self):
-        """Per-wave {start, queue drained, end, ray-steps} of the last k_trace (100 MHz ticks)."""
+        """Per-wave stamps of the last k_trace: {start, queue drained, end (100 MHz ticks),
+        iterations after drain << 32 | iterations, shader-clock cycles in refill, shading,
+        MLP, scene + step}."""
         n = ctypes.c_size_t()
         self._chk(self._L.nr_debug_stamps(self._ctx, None, 0, ctypes.byref(n)))
-        buf = np.zeros((n.value, 4), np.uint64)
+        buf = np.zeros((n.value, 8), np.uint64)
         self._chk(self._L.nr_debug_stamps(self._ctx, buf.ctypes.data, buf.size, ctypes.byref(n)))
         return buf
 

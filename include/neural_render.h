@@ -153,9 +153,14 @@ int nr_set_profiling(nr_ctx *ctx, int on);
 int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
 int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
- * {start, pixel queue drained, end, ray-steps}; nr_debug_stamps copies the last
- * frame's (4 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
- * schedule writes each hit pixel's iteration count instead of its colour. */
+ * {start, pixel queue drained, end (100 MHz), (wave iterations after the drain << 32) |
+ * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene + step};
+ * nr_debug_stamps copies the last
+ * frame's (8 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
+ * schedule writes each hit pixel's iteration count instead of its colour.  Bit 6 =
+ * MLP latency probe: nr_mlp_forward(X >= 64 points, Y >= 65 floats, n = repetitions, on
+ * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
+ * writes the shader cycles per evaluation to Y[0]. */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are
@@ -163,6 +168,14 @@ int nr_set_debug(nr_ctx *ctx, int flags);
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
+/* Rays per wave (persistent schedule, 1-64, default 64): a wave marches at most this
+ * many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or two
+ * 16-ray tiles -- shorter per-iteration latency for small frames or shards, where the
+ * longest ray rather than the matrix-core throughput sets the frame time. */
+int nr_set_wave_rays(nr_ctx *ctx, int rays);
+/* Pixel-queue shards (persistent schedule; power of two <= 64, default 8): the queue's
+ * atomic counters, each on its own 128-byte line, that the waves take pixels from. */
+int nr_set_queue_shards(nr_ctx *ctx, int n);
 /* Age hold (persistent schedule): a wave holding a ray that has marched `age` or more
  * iterations stops taking new pixels, packs its live rays into the fewest 16-ray tiles
  * and raises its issue priority to `prio` (0-3) until they finish, so long rays march

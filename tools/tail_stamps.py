@@ -20,22 +20,27 @@ ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--temporal", type=int, default=0)
 ap.add_argument("--spread", type=int, default=0)
 ap.add_argument("--hold", type=int, default=0)
+ap.add_argument("--nshards", type=int, default=1)
+ap.add_argument("--rays", type=int, default=64)
+ap.add_argument("--queues", type=int, default=8)
 a = ap.parse_args()
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
 r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(nr.load_png(nr.matcap_path("Chrome")))
 r.set_occupancy(a.bpc)
 r.set_temporal_order(a.temporal)
-r.set_pixel_spread(a.spread).set_age_hold(a.hold, 2)
+r.set_pixel_spread(a.spread).set_age_hold(a.hold, 2).set_wave_rays(a.rays).set_queue_shards(a.queues)
 for _ in range(3):
-    r.render(a.size, a.size, a.steps)
+    r.render_shard(a.size, a.size, 8, a.nshards, 0, a.steps)
 r.set_debug(1)
-img, st = r.render(a.size, a.size, a.steps)
+img, st = r.render_shard(a.size, a.size, 8, a.nshards, 0, a.steps)
 s = r.debug_stamps().astype(np.int64)
 s = s[s[:, 2] > 0]
 t0 = s[:, 0].min()
-start, empty, end, steps = (s[:, 0] - t0) / 100.0, s[:, 1], (s[:, 2] - t0) / 100.0, s[:, 3]
+start, empty, end = (s[:, 0] - t0) / 100.0, s[:, 1], (s[:, 2] - t0) / 100.0
+wit, wit_tail = s[:, 3] & 0xffffffff, s[:, 3] >> 32
 empty = np.where(empty > 0, (empty - t0) / 100.0, np.nan)
-print(f"== bpc {a.bpc} temporal {a.temporal} spread {a.spread} hold {a.hold} precision {a.precision}: stats {st}")
+print(f"== bpc {a.bpc} temporal {a.temporal} spread {a.spread} hold {a.hold} rays {a.rays} queues {a.queues} "
+      f"nshards {a.nshards} precision {a.precision}: stats {st}")
 print(f"waves {len(s)}  start spread {start.max():.1f} us  kernel span {end.max():.1f} us")
 print(f"queue drained: first {np.nanmin(empty):.1f} us  median {np.nanmedian(empty):.1f} us  last {np.nanmax(empty):.1f} us")
 q = np.percentile(end, [10, 50, 90, 99, 100])
@@ -45,3 +50,15 @@ print(f"tail after last drain: {end.max() - d:.1f} us ({(end.max() - d) / end.ma
       f" steps after drain-ish: waves ending > drain+50us: {(end > d + 50).sum()}")
 hist = np.histogram(end, bins=np.arange(0, end.max() + 100, 100))[0]
 print("waves ending per 100us bin:", hist.tolist())
+last = np.argsort(end)[-8:]
+for i in last:
+    tail_us = end[i] - empty[i] if not np.isnan(empty[i]) else float("nan")
+    print(f"  wave ending {end[i]:.1f} us: iterations {wit[i]} ({wit_tail[i]} after drain at {empty[i]:.1f} us), "
+          f"{(end[i] - start[i]) / max(wit[i], 1):.2f} us/iter overall, {tail_us / max(wit_tail[i], 1):.2f} us/iter after drain")
+ph = s[:, 4:8].astype(np.float64)
+tot = ph.sum(axis=1)
+print("phase share of wave cycles (refill, shading, MLP, scene+step), all waves:",
+      np.round(ph.sum(axis=0) / tot.sum(), 3).tolist())
+for i in last[-3:]:
+    print(f"  wave ending {end[i]:.1f} us: cycles/iter refill {ph[i,0]/max(wit[i],1):.0f} shading {ph[i,1]/max(wit[i],1):.0f} "
+          f"mlp {ph[i,2]/max(wit[i],1):.0f} scene+step {ph[i,3]/max(wit[i],1):.0f}")
