@@ -510,7 +510,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         if (c->debug & 1) {
-            if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 8 * 8));
+            if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 16 * 8));
             T.stamps = c->d_stamps;
             c->n_stamps = (size_t)grid * 4;
         }
@@ -680,7 +680,7 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 4;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
-            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, s));
+            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
         else if ((c->debug & 2) == 0)
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
         else  // 32-point-tile variant (k_mlp), kept for comparison
@@ -826,8 +826,8 @@ int nr_debug_stamps(nr_ctx *c, unsigned long long *out, size_t cap, size_t *n) {
         GET_STREAM(c, s_);
         HIPCHK(c, hipStreamSynchronize(s_));
     }
-    size_t m = std::min(cap / 8, c->n_stamps);
-    HIPCHK(c, hipMemcpy(out, c->d_stamps, m * 8 * 8, hipMemcpyDeviceToHost));
+    size_t m = std::min(cap / 16, c->n_stamps);
+    HIPCHK(c, hipMemcpy(out, c->d_stamps, m * 16 * 8, hipMemcpyDeviceToHost));
     return NR_OK;
 }
 

@@ -27,7 +27,8 @@ __device__ __forceinline__ float tile_outputs(const float zt[4]) {
 }
 
 // FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
-template <int NT>
+// PART != 0 only in the latency diagnostic (nr_diag.hip): stop after the hidden layers.
+template <int NT, int PART = 0>
 __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
                                                float y, float z) {
     // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
@@ -86,6 +87,7 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
     }
+    if constexpr (PART != 0) return a[0][0] + a[NT - 1][7];
     // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
     // groups 0 -> 1 -> 2 -> 3 with one cross-lane hand-off per group.
     const float *wf = s + pk_final(nh) + g * 8;

@@ -105,7 +105,10 @@ __device__ __forceinline__ void set_priority(int prio) {
 // PROBE: the cost-probe pre-pass (TraceArgs::probe) -- one ray per 8x8 block, at most
 // T.take rays per wave, no pixels written; each block's bcost gets its probe ray's
 // iteration count (max_steps is the probe's cap).
-template <int PREC, bool PROBE>
+// STAMPS: the diagnostic build (nr_set_debug bit 0) -- per-wave s_memrealtime stamps
+// and per-phase shader-clock counters; a separate instance so that the counters cost
+// the production kernel no registers.
+template <int PREC, bool PROBE, bool STAMPS = false>
 __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     Smem16 S = stage16(M, prec);
@@ -128,12 +131,12 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     bool live = false;
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
-    unsigned long long ph[4] = {0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene+step
-    const bool timing = T.stamps != nullptr;
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene, step
+    constexpr bool timing = STAMPS;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    unsigned long long t_start = T.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
+    unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
-        if (timing) tph = __builtin_amdgcn_s_memtime();
+        if constexpr (timing) tph = __builtin_amdgcn_s_memtime();
         // ---- refill free slots from the pixel queue
         if (!qempty && !(hold && !T.hold_refill)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
@@ -155,7 +158,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                     shard = (shard + 1) & (nq - 1);
                     if (++tries >= nq) {
                         qempty = true;
-                        if (T.stamps) t_empty = __builtin_amdgcn_s_memrealtime();
+                        if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
                         break;
                     }
                 }
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         // Once the queue is drained a partial pass waits until the wave's last ray has
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
         // its size, and the marching rays must not wait for it.
-        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
         uint64_t lm = __ballot(live);
         while (nstash >= 16 || (qempty && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             nconv += (uint64_t)nb;
             nstash -= nb;
         }
-        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; tph = t; }
         if (!lm) {
             if (qempty && nstash == 0) break;
             continue;
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr, p.x, p.y, p.z, tmask);
-        if (timing) {
+        if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
             ph[2] += t - tph; tph = t;
@@ -263,6 +266,11 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         bool conv = false;
         if (live) {
             const float ts = scene_sdf(p, sdf, A.scene, A.frame);
+            if constexpr (timing) {
+                __builtin_amdgcn_s_waitcnt(0);
+                const unsigned long long t = __builtin_amdgcn_s_memtime();
+                ph[3] += t - tph; tph = t;
+            }
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
             if (tfar <= 0) {
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             stash[wid][slot][1] = make_float4(d.x, d.y, d.z, 0.0f);
         }
         nstash += (int)__popcll(cm);
-        if (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[3] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; tph = t; }
         const bool h = __ballot(live && it >= T.hold_age) != 0;
         if (h != hold) {
             hold = h;
@@ -312,11 +320,11 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     // ---- frame statistics: one set of atomics per wave
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
-    if (T.stamps && lane == 0) {
-        unsigned long long *st = T.stamps + 8 * gwave;
+    if (STAMPS && lane == 0) {
+        unsigned long long *st = T.stamps + 16 * gwave;
         st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime();
         st[3] = ((unsigned long long)wit_tail << 32) | wit;
-        st[4] = ph[0]; st[5] = ph[1]; st[6] = ph[2]; st[7] = ph[3];
+        for (int i = 0; i < 5; ++i) st[4 + i] = ph[i];
     }
     if (lane == 0) {
         if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
@@ -348,35 +356,6 @@ __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__rest
         const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask);
         if (live) Y[i] = v;
     }
-}
-
-// Diagnostic (nr_set_debug bit 6): latency of the fp32 MLP on NT tiles for one wave
-// alone on its SIMD -- `reps` back-to-back evaluations, each input depending on the
-// previous output.  Y[0] = shader cycles per evaluation, Y[1..64] = the last outputs.
-template <int NT>
-__global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
-                                                    int reps) {
-    Smem16 S = stage16(M, NR_PRECISION_FP32);
-    const int lane = lane_id();
-    float x = X[3 * lane], y = X[3 * lane + 1], z = X[3 * lane + 2], v = 0.0f;
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    for (int r = 0; r < reps; ++r) {
-        v = mlp16_fp32_nt<NT>(S.s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
-    Y[1 + lane] = v;
-}
-
-hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st) {
-    const int sm = smem_bytes(M, NR_PRECISION_FP32);
-    if (nt <= 1) hipLaunchKernelGGL(k_mlp_latency<1>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 2) hipLaunchKernelGGL(k_mlp_latency<2>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 3) hipLaunchKernelGGL(k_mlp_latency<3>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else hipLaunchKernelGGL(k_mlp_latency<4>, dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    return hipGetLastError();
 }
 
 // Counting sort of the blocks by their cost, descending (one workgroup): the order in
@@ -438,6 +417,13 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+    } else if (T.stamps) {
+        if (prec == NR_PRECISION_BF16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
     } else {
         if (prec == NR_PRECISION_BF16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false>), dim3(grid), dim3(256), sm, st, A, M, T);

@@ -154,13 +154,14 @@ int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
 int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
  * {start, pixel queue drained, end (100 MHz), (wave iterations after the drain << 32) |
- * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene + step};
+ * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene, step, -};
  * nr_debug_stamps copies the last
- * frame's (8 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
+ * frame's (16 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
  * schedule writes each hit pixel's iteration count instead of its colour.  Bit 6 =
  * MLP latency probe: nr_mlp_forward(X >= 64 points, Y >= 65 floats, n = repetitions, on
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
- * writes the shader cycles per evaluation to Y[0]. */
+ * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
+ * layer. */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are

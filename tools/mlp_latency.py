@@ -13,11 +13,15 @@ import cudaneuralrender_amd as nr  # noqa: E402
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 X = torch.from_numpy(np.random.default_rng(0).uniform(-1, 1, (64, 3)).astype(np.float32)).cuda()
 Y = torch.zeros(65, dtype=torch.float32, device="cuda")
-r.set_debug(64)
-for nt in (1, 2, 3, 4):
-    r.set_wave_rays(16 * nt)
-    for _ in range(2):
-        r.mlp_forward_device(X.data_ptr(), Y.data_ptr(), 2000)
-    torch.cuda.synchronize()
-    cyc = float(Y[0].item())
-    print(f"tiles {nt}: {cyc:.0f} cycles per MLP ({cyc / nt:.0f} per tile; MFMA issue floor {114 * 32 * nt})", flush=True)
+# (the no-final-layer variant is meaningful for 1-2 tiles only: with more, the tiles whose
+# outputs it drops are dead code)
+for part, name in [(0, "full"), (1, "no final layer")]:
+    r.set_debug(64 | (part << 7))
+    for nt in (1, 2, 3, 4):
+        r.set_wave_rays(16 * nt)
+        for _ in range(2):
+            r.mlp_forward_device(X.data_ptr(), Y.data_ptr(), 2000)
+        torch.cuda.synchronize()
+        cyc = float(Y[0].item())
+        print(f"{name:18s} tiles {nt}: {cyc:.0f} cycles per MLP ({cyc / nt:.0f} per tile; "
+              f"MFMA issue floor {114 * 32 * nt})", flush=True)

@@ -55,10 +55,10 @@ for i in last:
     tail_us = end[i] - empty[i] if not np.isnan(empty[i]) else float("nan")
     print(f"  wave ending {end[i]:.1f} us: iterations {wit[i]} ({wit_tail[i]} after drain at {empty[i]:.1f} us), "
           f"{(end[i] - start[i]) / max(wit[i], 1):.2f} us/iter overall, {tail_us / max(wit_tail[i], 1):.2f} us/iter after drain")
-ph = s[:, 4:8].astype(np.float64)
+ph = s[:, 4:9].astype(np.float64)
 tot = ph.sum(axis=1)
-print("phase share of wave cycles (refill, shading, MLP, scene+step), all waves:",
+print("phase share of wave cycles (refill, shading, MLP, scene, step), all waves:",
       np.round(ph.sum(axis=0) / tot.sum(), 3).tolist())
 for i in last[-3:]:
     print(f"  wave ending {end[i]:.1f} us: cycles/iter refill {ph[i,0]/max(wit[i],1):.0f} shading {ph[i,1]/max(wit[i],1):.0f} "
-          f"mlp {ph[i,2]/max(wit[i],1):.0f} scene+step {ph[i,3]/max(wit[i],1):.0f}")
+          f"mlp {ph[i,2]/max(wit[i],1):.0f} scene {ph[i,3]/max(wit[i],1):.0f} step {ph[i,4]/max(wit[i],1):.0f}")

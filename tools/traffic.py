@@ -16,7 +16,7 @@ def per_dispatch(counter_dir, name):
     vals = []
     for f in glob.glob(f"{counter_dir}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_trace<0, false>" in r["Kernel_Name"] and r["Counter_Name"] == name:
+            if "k_trace<0, false, false>" in r["Kernel_Name"] and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals), len(vals)
 
@@ -25,7 +25,7 @@ fetch, nf = per_dispatch(f"{out}/fetch", "FETCH_SIZE")
 write, nw = per_dispatch(f"{out}/write", "WRITE_SIZE")
 hbm = fetch * 1024 * 2 + write * 1024
 print(json.dumps({
-    "kernel": "k_trace<0, false> (fp32)",
+    "kernel": "k_trace<0, false, false> (fp32)",
     "workload": "plane_1 1024x1024, 128 march steps, fp32, Chrome.png, v1 scene, default camera",
     "collection": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, tools/render_frames.py --frames 3",
     "dispatches": [nf, nw],
