@@ -21,7 +21,7 @@ NR_SCHEDULE = {"persistent": 0, "wavefront": 1}
 EXPORTS = [
     "nr_create", "nr_destroy", "nr_last_error", "nr_abi_version", "nr_set_stream", "nr_synchronize",
     "nr_load_h5", "nr_load_mlp", "nr_mlp_info", "nr_set_precision", "nr_set_view", "nr_set_static",
-    "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_shard_rows",
+    "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_render_batch", "nr_shard_rows",
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
@@ -42,6 +42,16 @@ class NRStats(ctypes.Structure):
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class NRFrame(ctypes.Structure):
+    """nr_frame: one frame of nr_render_batch."""
+    _fields_ = [
+        ("inv_view", ctypes.c_float * 12),
+        ("normal", ctypes.c_float * 16),
+        ("frame", ctypes.c_int),
+        ("out", ctypes.c_void_p),
+    ]
 
 
 class NRKernelProf(ctypes.Structure):
@@ -96,6 +106,7 @@ def lib():
         "nr_set_matcap": (I, [P, P, I, I]),
         "nr_render": (I, [P, P, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_render_shard": (I, [P, P, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
+        "nr_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_shard_rows": (I, [I, I, I, I]),
         "nr_assemble_shards": (I, [P, P, ctypes.c_size_t, P, I, I, I, I, I]),
         "nr_mlp_forward": (I, [P, P, P, L64, I]),

@@ -57,6 +57,12 @@ struct nr_ctx {
     int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
     int wave_rays = 64;  // nr_set_wave_rays
     int nq_shift = 3;    // nr_set_queue_shards: 8
+    // nr_render_batch: per-frame arguments (pinned staging + device copy), host-output scratch
+    FrameArgs *h_frames = nullptr, *d_frames = nullptr;
+    size_t cap_frames = 0;
+    hipEvent_t ev_frames = nullptr;
+    uint32_t *d_bout = nullptr;
+    size_t cap_bout = 0;
     uint32_t *d_bcost = nullptr, *d_order[2] = {nullptr, nullptr};
     size_t cap_blocks = 0;
     int order_valid = 0, order_cur = 0;
@@ -200,6 +206,9 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
 int ensure_rays(nr_ctx *c, size_t n) {
     if (n <= c->cap_rays) return NR_OK;
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
+    if (c->h_frames) (void)hipHostFree(c->h_frames);
+    if (c->ev_frames) (void)hipEventDestroy(c->ev_frames);
+    dfree(c->d_frames); dfree(c->d_bout);
     dfree(c->d_SP); dfree(c->d_SD);
     c->cap_rays = 0;
     size_t b = std::max<size_t>(n, 64) * sizeof(float4);
@@ -420,6 +429,142 @@ int nr_set_matcap(nr_ctx *c, const uint32_t *rgba, int w, int h) {
     HIPCHK(c, hipMalloc(&c->d_matcap, (size_t)w * h * 4));
     HIPCHK(c, hipMemcpy(c->d_matcap, rgba, (size_t)w * h * 4, hipMemcpyHostToDevice));
     c->mw = w; c->mh = h;
+    return NR_OK;
+}
+
+int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H, int band, int nshards, int shard,
+                    int max_steps, int loc, nr_stats *stats) {
+    if (!c || !frames || nframes < 1) return set_err(c, NR_E_INVALID, "nr_render_batch: bad arguments");
+    for (int i = 0; i < nframes; ++i)
+        if (!frames[i].out) return set_err(c, NR_E_INVALID, "nr_render_batch: frame %d has no output", i);
+    if (W < 1 || H < 1 || (long)W * H > (1l << 31)) return set_err(c, NR_E_INVALID, "nr_render: bad size %dx%d", W, H);
+    if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
+    if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
+    if (c->schedule != NR_SCHED_PERSISTENT || (c->debug & (1 | 8))) {
+        // frame by frame (the wavefront schedule and the diagnostics are single-frame)
+        float iv[12], nm[16];
+        memcpy(iv, c->inv_view, sizeof iv);
+        memcpy(nm, c->normal, sizeof nm);
+        const int fr0 = c->frame;
+        nr_stats tot{};
+        int rc = NR_OK;
+        for (int i = 0; i < nframes && rc == NR_OK; ++i) {
+            memcpy(c->inv_view, frames[i].inv_view, sizeof iv);
+            memcpy(c->normal, frames[i].normal, sizeof nm);
+            c->frame = frames[i].frame;
+            nr_stats st{};
+            rc = nr_render_shard(c, frames[i].out, W, H, band, nshards, shard, max_steps, loc, stats ? &st : nullptr);
+            tot.ray_steps += st.ray_steps; tot.shade_evals += st.shade_evals; tot.rays_hit += st.rays_hit;
+            tot.rays_shaded += st.rays_shaded; tot.iterations = std::max(tot.iterations, st.iterations);
+            tot.launches += st.launches; tot.ms_total += st.ms_total;
+        }
+        memcpy(c->inv_view, iv, sizeof iv);
+        memcpy(c->normal, nm, sizeof nm);
+        c->frame = fr0;
+        if (rc == NR_OK && stats) *stats = tot;
+        return rc;
+    }
+    if (c->dims.empty()) return set_err(c, NR_E_STATE, "nr_render: no network loaded");
+    if (!c->fused)
+        return set_err(c, NR_E_FORMAT, "nr_render: network shape unsupported by the fused march kernel "
+                                       "(needs [3|4, 32, ..., 32, 1])");
+    if (c->dims[0] != c->num_inputs)
+        return set_err(c, NR_E_STATE, "nr_render: network takes %d inputs but numInputs = %d", c->dims[0], c->num_inputs);
+    if (c->color_type == NR_COLOR_MATCAP && !c->d_matcap) return set_err(c, NR_E_STATE, "nr_render: matcap colouring without a matcap");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int rows = nr_shard_rows(H, band, nshards, shard);
+    const size_t npix = (size_t)W * rows;
+    nr_stats st{};
+    if (npix == 0) { if (stats) *stats = st; return NR_OK; }
+    GET_STREAM(c, s);
+    int rc;
+    // per-frame arguments: pinned staging (reused only once the previous upload is done)
+    if (!c->ev_frames) HIPCHK(c, hipEventCreateWithFlags(&c->ev_frames, hipEventDisableTiming));
+    HIPCHK(c, hipEventSynchronize(c->ev_frames));
+    if ((size_t)nframes > c->cap_frames) {
+        if (c->h_frames) HIPCHK(c, hipHostFree(c->h_frames));
+        dfree(c->d_frames);
+        c->h_frames = nullptr;
+        c->cap_frames = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_frames, (size_t)nframes * sizeof(FrameArgs)));
+        HIPCHK(c, hipMalloc(&c->d_frames, (size_t)nframes * sizeof(FrameArgs)));
+        c->cap_frames = nframes;
+    }
+    const int chunk = std::min(nframes, NR_MAX_BATCH);
+    if (loc != NR_DEVICE && (rc = ensure_buf(c, c->d_bout, c->cap_bout, npix * chunk)) != NR_OK) return rc;
+    for (int i = 0; i < nframes; ++i) {
+        FrameArgs &f = c->h_frames[i];
+        memcpy(f.inv_view, frames[i].inv_view, sizeof f.inv_view);
+        memcpy(f.normal, frames[i].normal, sizeof f.normal);
+        f.zoff = -0.7 + ((double)(frames[i].frame * 2) * 0.7 / 360.0);  // sphere_zoff, same f64 ops
+        f.frame = frames[i].frame;
+        f.frame_f = (float)frames[i].frame;
+        f.out = loc == NR_DEVICE ? frames[i].out : c->d_bout + (size_t)(i % chunk) * npix;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_frames, c->h_frames, (size_t)nframes * sizeof(FrameArgs), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipEventRecord(c->ev_frames, s));
+
+    RenderArgs A{};
+    A.out = nullptr; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
+    A.max_steps = max_steps; A.scene = c->scene; A.frame = 0; A.color_type = c->color_type;
+    A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    const size_t tr_bytes = NR_MAX_QUEUES * 128 + 4 * 8;
+    if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
+    TraceArgs T{};
+    T.pix_ctr = c->d_tr;
+    T.stats = reinterpret_cast<unsigned long long *>(c->d_tr + NR_MAX_QUEUES * 32);
+    T.nq_shift = c->nq_shift;
+    T.bw = (W + 7) / 8;
+    T.nblocks = T.bw * ((rows + 7) / 8);
+    T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
+    T.hold_prio = c->hold_prio & 3;
+    T.hold_refill = c->hold_prio >= 4;
+    T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
+    T.inv_bw = 1.0 / (double)T.bw;
+    T.inv_band = 1.0 / (double)band;
+    T.take = c->wave_rays;
+    T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
+    const int cus = num_cus(c->device);
+    const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    int launches = 0;
+    for (int f0 = 0; f0 < nframes; f0 += chunk) {
+        const int n = std::min(chunk, nframes - f0);
+        T.frames = c->d_frames + f0;
+        T.nframes = n;
+        // the counters restart for every launch; the statistics accumulate
+        HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
+        int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
+        if (grid < 1) grid = 1;
+        int rc2;
+        if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
+        HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
+        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        ++launches;
+        if (loc != NR_DEVICE)
+            for (int i = f0; i < f0 + n; ++i)
+                HIPCHK(c, hipMemcpyAsync(frames[i].out, c->d_bout + (size_t)(i % chunk) * npix, npix * 4,
+                                         hipMemcpyDeviceToHost, s));
+    }
+    if (c->profiling) c->prof_renders += nframes;
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    if (stats) {
+        unsigned long long hs[4];
+        HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        st.ray_steps = hs[0];
+        st.rays_hit = hs[1];
+        st.iterations = (int32_t)hs[2];
+        st.rays_shaded = hs[3];
+        st.shade_evals = 4ull * hs[3];
+        st.launches = launches;
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        st.ms_total = ms;
+        *stats = st;
+    } else if (loc != NR_DEVICE) {
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
     return NR_OK;
 }
 

@@ -110,7 +110,10 @@ __device__ __forceinline__ float smooth_union(float d1, float d2, float k) {  //
     return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
 }
 
-__device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
+// z offset of the sphere grid in frame `frame` (cP.z += ..., :184), in f64 as the reference
+__device__ __forceinline__ double sphere_zoff(int frame) { return -0.7 + ((double)(frame * 2) * 0.7 / 360.0); }
+
+__device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
     // the x values repeat in every row, so the 3 x, 3 y and 1 z coordinates are formed
@@ -122,7 +125,7 @@ __device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
     const float y0 = (float)((double)ys + 0.4);
     const float y1 = (float)((double)y0 + 0.4);
     const float y2 = (float)((double)y1 + 0.4);
-    const float zc = (float)((double)p.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+    const float zc = (float)((double)p.z + zoff);
     const float xx[3] = {x0 * x0, x1 * x1, x2 * x2};
     const float yy[3] = {y0 * y0, y1 * y1, y2 * y2};
     const float zz = zc * zc;
@@ -146,9 +149,9 @@ __device__ float many_sphere(F3 p, float nsdf, int frame) {  // :176-196
     return s;
 }
 
-__device__ __forceinline__ float scene_sdf(F3 p, float nsdf, int scene, int frame) {  // :217-230
+__device__ __forceinline__ float scene_sdf(F3 p, float nsdf, int scene, double zoff) {  // :217-230
     if (scene == NR_SCENE_TANH) return nr_tanh(nsdf);
-    return many_sphere(p, nsdf, frame);
+    return many_sphere(p, nsdf, zoff);
 }
 
 __device__ __forceinline__ uint32_t rgba_to_uint(float r, float g, float b, float a) {  // :266-274
@@ -157,16 +160,17 @@ __device__ __forceinline__ uint32_t rgba_to_uint(float r, float g, float b, floa
            (uint32_t)(r * 255);
 }
 
-__device__ uint32_t shade_color(const RenderArgs &A, F3 n, F3 d) {
+// nm: the frame's normal matrix (c_normalMatrix, row-major 4x4)
+__device__ uint32_t shade_color(const RenderArgs &A, const float *nm, F3 n, F3 d) {
     if (A.color_type == NR_COLOR_FACING) {  // facingColor :380-384
         float dd = dot3(n, mk3(-d.x, -d.y, -d.z));
         float ratio = (dd > 0.0f) ? dd : 0.0f;
         return rgba_to_uint(ratio, ratio, ratio, 1.0f);
     }
     // matCapColor :387-413
-    float ex = dot4(n.x, n.y, n.z, 0.0f, A.normal + 0);
-    float ey = dot4(n.x, n.y, n.z, 0.0f, A.normal + 4);
-    float ez = dot4(n.x, n.y, n.z, 0.0f, A.normal + 8);
+    float ex = dot4(n.x, n.y, n.z, 0.0f, nm + 0);
+    float ey = dot4(n.x, n.y, n.z, 0.0f, nm + 4);
+    float ez = dot4(n.x, n.y, n.z, 0.0f, nm + 8);
     F3 ne = normalize3(mk3(ex, ey, ez));
     float fuvx = (float)((double)ne.x * 0.5 + 0.5);
     float fuvy = (float)((double)ne.y * 0.5 + 0.5);

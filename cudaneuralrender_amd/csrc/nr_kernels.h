@@ -38,6 +38,18 @@ struct QueueArgs {
 };
 
 // Persistent-schedule state (nr_trace.hip).
+// One frame of a batched launch (nr_render_batch): its camera, sphere-grid offset,
+// animation input and output image.  Staged into LDS by k_trace<.., BATCH>.
+struct FrameArgs {
+    float inv_view[12];
+    float normal[16];
+    double zoff;        // sphere_zoff(frame)
+    uint32_t *out;
+    float frame_f;      // the network's 4th input when it takes one
+    int frame;
+};
+constexpr int NR_MAX_BATCH = 32;
+
 struct TraceArgs {
     uint32_t *pix_ctr;          // 2^nq_shift pixel-queue shard counters, one per 128-byte line (stride 32)
     int nq_shift;
@@ -59,7 +71,9 @@ struct TraceArgs {
     double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r
     // cost probe (k_trace<.., true>): one ray per block
     int probe, take;
-    uint64_t lane_cap;          // lanes a wave may fill: (1 << take) - 1, all 64 for take = 64                  // diagnostics: write each pixel's iteration count instead of its colour
+    uint64_t lane_cap;          // lanes a wave may fill: (1 << take) - 1, all 64 for take = 64
+    const FrameArgs *frames;    // batched launch: nframes frames (k_trace<.., BATCH>)
+    int nframes;                  // diagnostics: write each pixel's iteration count instead of its colour
 };
 
 int smem_bytes(const MlpArgs &M, int prec);

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void k_march(RenderArgs A, MlpArgs M, QueueArg
         F3 p = mk3(sp.x, sp.y, sp.z);
         float tfar = sp.w;
         if (live) {
-            float tstep = scene_sdf(p, sdf, A.scene, A.frame);
+            float tstep = scene_sdf(p, sdf, A.scene, sphere_zoff(A.frame));
             tfar -= tstep;
             if (tfar <= 0) {
                 // background: output already 0
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(256) void k_shade(RenderArgs A, MlpArgs M, QueueArg
         F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
         F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
         float sdf = mlp_fp32_wave(S.s32, M.in0, M.nh, pq.x, pq.y, pq.z, fr);
-        F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, A.frame));
+        F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sphere_zoff(A.frame)));
         const int l0 = lane & ~3;
         float c1x = __shfl(cq.x, l0 + 1), c1y = __shfl(cq.y, l0 + 1), c1z = __shfl(cq.z, l0 + 1);
         float c2x = __shfl(cq.x, l0 + 2), c2y = __shfl(cq.y, l0 + 2), c2z = __shfl(cq.z, l0 + 2);
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_shade(RenderArgs A, MlpArgs M, QueueArg
             F3 acc = add3(add3(add3(cq, mk3(c1x, c1y, c1z)), mk3(c2x, c2y, c2z)), mk3(c3x, c3y, c3z));
             F3 nrm = normalize3(acc);
             uint32_t pix = __float_as_uint(sd.w);
-            A.out[pix] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
+            A.out[pix] = shade_color(A, A.normal, nrm, mk3(sd.x, sd.y, sd.z));
         }
     }
 }

@@ -63,14 +63,13 @@ __device__ __forceinline__ uint32_t udiv_r(uint32_t n, uint32_t d, double inv_d)
 
 // Ray generation for pixel x of local row lr of the shard (initMarcher :293-358).
 // Returns hit.
-__device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T, int x, int lr, F3 &p, F3 &d,
-                                        float &tfar) {
+__device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T, const float *M, int x, int lr,
+                                        F3 &p, F3 &d, float &tfar) {
     int y = lr;
     if (A.nshards > 1) {
         const int bi = (int)udiv_r((uint32_t)lr, (uint32_t)A.band, T.inv_band);
         y = (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
     }
-    const float *M = A.inv_view;
     F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
                dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
     float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
@@ -108,15 +107,31 @@ __device__ __forceinline__ void set_priority(int prio) {
 // STAMPS: the diagnostic build (nr_set_debug bit 0) -- per-wave s_memrealtime stamps
 // and per-phase shader-clock counters; a separate instance so that the counters cost
 // the production kernel no registers.
-template <int PREC, bool PROBE, bool STAMPS = false>
+// BATCH: T.nframes frames in one launch (nr_render_batch).  The pixel queue runs through
+// the frames one after another, so one frame's longest rays march while the next
+// frame's pixels fill the freed slots; every ray carries its frame index (rf) and the
+// frame-dependent values (camera, sphere offset, animation input, output image) come
+// from the FrameArgs staged in LDS.
+template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
 __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
-    Smem16 S = stage16(M, prec);
+    __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
+    if constexpr (BATCH) {
+        const int nw = T.nframes * (int)(sizeof(FrameArgs) / 4);
+        for (int i = threadIdx.x; i < nw; i += blockDim.x)
+            reinterpret_cast<uint32_t *>(sf)[i] = reinterpret_cast<const uint32_t *>(T.frames)[i];
+    }
+    Smem16 S = stage16(M, prec);  // (its __syncthreads also covers sf)
     __shared__ float4 stash[4][STASH][2];  // per wave: {p.xyz, pixel}, {d.xyz, -}
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
     const float fr = (float)A.frame;
+    const double zoff0 = sphere_zoff(A.frame);
+    // frame-dependent values of frame f (single-frame launches: the uniform ones in A)
+    auto out_of = [&](int f) -> uint32_t * { return BATCH ? sf[f].out : A.out; };
+    auto zoff_of = [&](int f) -> double { return BATCH ? sf[f].zoff : zoff0; };
+    auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
     const int q4 = lane & 3;
     const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
     int nstash = 0;
@@ -127,6 +142,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
     float tfar = 0.0f;
     uint32_t pix = 0;
+    int rf = 0;  // the ray's frame (BATCH)
     int it = 0, maxit = 0;
     bool live = false;
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
@@ -147,7 +163,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                 uint32_t base = 0, got = 0;
                 while (true) {
                     const long sh_chunks = shard < nchunks ? ((nchunks - 1 - shard) >> T.nq_shift) + 1 : 0;
-                    const long total = PROBE ? sh_chunks : sh_chunks * 64;
+                    const long total = (PROBE ? sh_chunks : sh_chunks * 64) * (BATCH ? T.nframes : 1);
                     uint32_t b = 0;
                     if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
                     base = __shfl(b, 0);
@@ -166,7 +182,13 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                     const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
                     bool hit = false;
                     if (!live && rank < got) {
-                        const uint32_t q = base + rank;
+                        uint32_t q = base + rank;
+                        int f = 0;
+                        if constexpr (BATCH) {  // frame-major: frame f owns [f * per, (f + 1) * per)
+                            const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
+                            f = (int)udiv_r(q, per, 1.0 / (double)per);
+                            q -= (uint32_t)f * per;
+                        }
                         uint32_t bq = q >> 6, pq = q & 63;
                         if (PROBE) {
                             bq = q;
@@ -190,13 +212,14 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                         }
                         const long lp = (long)py * A.W + px;
                         if (px < A.W && py < A.rows) {
-                            hit = gen_ray(A, T, px, py, p, d, tfar);
+                            hit = gen_ray(A, T, BATCH ? sf[f].inv_view : A.inv_view, px, py, p, d, tfar);
                             if (hit && A.max_steps > 0) {
                                 live = true;
                                 it = 0;
                                 pix = (uint32_t)lp;
+                                rf = f;
                             } else if (!PROBE) {
-                                A.out[lp] = 0u;  // background (:335-339) or no iterations at all
+                                out_of(f)[lp] = 0u;  // background (:335-339) or no iterations at all
                             }
                         }
                     }
@@ -216,17 +239,19 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             const int e = nstash - nb + (k < nb ? k : 0);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             const float4 sp = stash[wid][e][0], sd = stash[wid][e][1];
+            const int sfr = BATCH ? __float_as_int(sd.w) : 0;
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
-            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr, pq.x, pq.y, pq.z, smask);
-            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, A.frame));
+            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr_of(sfr), pq.x, pq.y, pq.z, smask);
+            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
             const int l0 = lane & ~3;
             const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
             const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
             const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
             if (k < nb && q4 == 0 && !T.itmap) {
                 const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                A.out[__float_as_uint(sp.w)] = shade_color(A, nrm, mk3(sd.x, sd.y, sd.z));
+                out_of(sfr)[__float_as_uint(sp.w)] =
+                    shade_color(A, BATCH ? sf[sfr].normal : A.normal, nrm, mk3(sd.x, sd.y, sd.z));
             }
             nconv += (uint64_t)nb;
             nstash -= nb;
@@ -247,6 +272,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                 d = mk3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
                 tfar = __shfl(tfar, src);
                 pix = (uint32_t)__shfl((int)pix, src);
+                if constexpr (BATCH) rf = __shfl(rf, src);
                 it = __shfl(it, src);
                 live = lane < nl;
                 lm = __ballot(live);
@@ -254,7 +280,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             }
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
-        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr, p.x, p.y, p.z, tmask);
+        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -265,7 +291,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         wit_tail += qempty ? 1u : 0u;
         bool conv = false;
         if (live) {
-            const float ts = scene_sdf(p, sdf, A.scene, A.frame);
+            const float ts = scene_sdf(p, sdf, A.scene, zoff_of(rf));
             if constexpr (timing) {
                 __builtin_amdgcn_s_waitcnt(0);
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -274,7 +300,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
             if (tfar <= 0) {
-                if (!PROBE) A.out[pix] = 0u;
+                if (!PROBE) out_of(rf)[pix] = 0u;
                 live = false;
                 used = it + 1;
             } else {
@@ -285,18 +311,18 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
                         conv = !PROBE;
                         used = it + 2;
                     } else {
-                        if (!PROBE) A.out[pix] = 0u;
+                        if (!PROBE) out_of(rf)[pix] = 0u;
                         used = it + 1;
                     }
                 } else if (++it >= A.max_steps) {  // iteration cap: pixel stays 0 (:690)
-                    if (!PROBE) A.out[pix] = 0u;
+                    if (!PROBE) out_of(rf)[pix] = 0u;
                     live = false;
                     used = A.max_steps;
                 }
             }
             if (used) {
                 maxit = max(maxit, used);
-                if (!PROBE && T.itmap) A.out[pix] = (uint32_t)used;
+                if (!PROBE && T.itmap) out_of(rf)[pix] = (uint32_t)used;
                 if (T.bcost) {
                     const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
                     atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
@@ -307,7 +333,7 @@ __global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, Trace
         if (conv) {
             const int slot = nstash + (int)__popcll(cm & lanemask_lt());
             stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
-            stash[wid][slot][1] = make_float4(d.x, d.y, d.z, 0.0f);
+            stash[wid][slot][1] = make_float4(d.x, d.y, d.z, __int_as_float(rf));
         }
         nstash += (int)__popcll(cm);
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; tph = t; }
@@ -417,6 +443,13 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+    } else if (T.nframes > 0) {
+        if (prec == NR_PRECISION_BF16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP16)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
     } else if (T.stamps) {
         if (prec == NR_PRECISION_BF16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);

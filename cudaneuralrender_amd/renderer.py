@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_HOST, NR_PRECISION, NR_SCENE, NR_SCHEDULE,
-                   NRKernelProf, NRStats, check, lib)
+                   NRFrame, NRKernelProf, NRStats, check, lib)
 
 _FP = ctypes.POINTER(ctypes.c_float)
 
@@ -260,6 +260,37 @@ class Renderer:
         st = NRStats()
         self._chk(self._L.nr_render(self._ctx, ctypes.c_void_p(out_ptr), W, H, max_steps, NR_DEVICE,
                                     ctypes.byref(st) if with_stats else None))
+        return st.as_dict() if with_stats else None
+
+    @staticmethod
+    def _frames(cams, outs):
+        fr = (NRFrame * len(cams))()
+        for i, (cam, o) in enumerate(zip(cams, outs)):
+            iv, nm = cam[0], cam[1]
+            fr[i].inv_view[:] = [float(v) for v in np.asarray(iv, np.float32).reshape(-1)]
+            fr[i].normal[:] = [float(v) for v in np.asarray(nm, np.float32).reshape(-1)]
+            fr[i].frame = int(cam[2]) if len(cam) > 2 else 0
+            fr[i].out = o
+        return fr
+
+    def render_batch(self, W, H, cams, max_steps=6000, band=8, nshards=1, shard=0, with_stats=True):
+        """nr_render_batch to host images: cams = [(inv_view, normal[, frame]), ...].
+        Returns the list of (rows, W) images (and the summed stats)."""
+        rows = shard_rows(H, band, nshards, shard)
+        outs = [np.zeros((rows, W), np.uint32) for _ in cams]
+        fr = self._frames(cams, [o.ctypes.data for o in outs])
+        st = NRStats()
+        self._chk(self._L.nr_render_batch(self._ctx, fr, len(cams), W, H, band, nshards, shard, max_steps, NR_HOST,
+                                          ctypes.byref(st) if with_stats else None))
+        return (outs, st.as_dict()) if with_stats else outs
+
+    def render_batch_device(self, out_ptrs, W, H, cams, max_steps=6000, band=8, nshards=1, shard=0,
+                            with_stats=False):
+        """nr_render_batch into device buffers (one per camera)."""
+        fr = self._frames(cams, list(out_ptrs))
+        st = NRStats()
+        self._chk(self._L.nr_render_batch(self._ctx, fr, len(cams), W, H, band, nshards, shard, max_steps, NR_DEVICE,
+                                          ctypes.byref(st) if with_stats else None))
         return st.as_dict() if with_stats else None
 
     def render_shard(self, W, H, band, nshards, shard, max_steps=6000, with_stats=True):

@@ -118,6 +118,24 @@ int nr_render(nr_ctx *ctx, uint32_t *out, int W, int H, int max_steps, int out_l
  * of nr_render. */
 int nr_render_shard(nr_ctx *ctx, uint32_t *out, int W, int H, int band_rows,
                     int nshards, int shard, int max_steps, int out_loc, nr_stats *stats);
+
+/* Batched frames (persistent schedule): render nframes frames -- each with its own camera
+ * (the nr_set_view matrices), frame number and output image -- of the same size/shard
+ * in as few launches as possible (up to 32 frames per launch).  The pixel queue runs
+ * through the frames in order, so one frame's longest rays march while the next
+ * frame's pixels keep the matrix cores busy: the throughput form of a sequence of
+ * nr_render_shard calls, with identical pixels.  The network, precision, scene,
+ * colouring and matcap are the context's.  `out` is a device or host pointer per `loc`;
+ * stats are summed over the frames.  Schedules other than persistent, and the debug
+ * flags 1 and 8, render frame by frame. */
+typedef struct nr_frame {
+    float inv_view[12];
+    float normal[16];
+    int frame;
+    uint32_t *out;
+} nr_frame;
+int nr_render_batch(nr_ctx *ctx, const nr_frame *frames, int nframes, int W, int H, int band, int nshards,
+                    int shard, int max_steps, int loc, nr_stats *stats);
 int nr_shard_rows(int H, int band_rows, int nshards, int shard);
 /* Re-interleave gathered shards (shard s's rows at src + s*stride_pixels) into a full
  * frame.  Host or device buffers (loc applies to both). */

@@ -256,3 +256,42 @@ def test_iteration_map(rend, nets, chrome):
     assert int(m.astype(np.int64).sum()) == st["ray_steps"] + st["rays_shaded"]
     assert m.max() == st["iterations"] <= 128
     assert ((m > 0) | (img == 0)).all()
+
+
+@pytest.mark.parametrize("nshards,shard,n", [(1, 0, 5), (3, 1, 3), (1, 0, 40)])
+def test_render_batch_matches_single_frames(rend, nets, chrome, nshards, shard, n):
+    """nr_render_batch: frames with their own cameras and frame numbers, in one launch
+    (40 frames: two launches), give each frame's single-frame pixels and summed stats."""
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
+    rend.set_matcap(chrome)
+    rng = np.random.default_rng(7)
+    cams = []
+    for i in range(n):
+        iv, nm = nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0)
+        cams.append((iv, nm, int(rng.integers(0, 360))))
+    W, H = 96, 77
+    imgs, st = rend.render_batch(W, H, cams, 128, band=8, nshards=nshards, shard=shard)
+    tot = 0
+    for (iv, nm, fr), img in zip(cams, imgs):
+        rend.set_view(iv, nm, fr)
+        ref, rst = rend.render_shard(W, H, 8, nshards, shard, 128)
+        assert np.array_equal(img, ref)
+        tot += rst["ray_steps"]
+    assert st["ray_steps"] == tot
+    rend.set_view(*nr.camera(0, 0, 2), 0)
+
+
+def test_render_batch_animation_vs_oracle(rend, nets, chrome):
+    """A batch of an animation (the sphere grid moves with the frame number) equals the
+    oracle frame by frame."""
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
+    rend.set_matcap(chrome)
+    iv, nm = nr.camera(-15.0, 40.0, 2.0)
+    cams = [(iv, nm, f) for f in (0, 90, 180)]
+    W, H = 64, 64
+    imgs, _ = rend.render_batch(W, H, cams, 128)
+    for (iv_, nm_, f), img in zip(cams, imgs):
+        ref, _ = oracle.OracleNet(K, B).render(W, H, iv_, nm_, frame=f, color_type=1, matcap=chrome, max_steps=128)
+        assert np.array_equal(img, ref)
