@@ -3,20 +3,25 @@
 BASELINE.json metric "Mray-steps/s + frames/s at 1024^2, plane_1.h5, 1/2/4/8 MI355X";
 workload = configs[1]: plane_1.h5, 1024x1024, 128 march steps, fp32, Chrome.png matcap,
 default camera (rx = ry = 0, zoom 2, frame 0), v1 scene (sceneSDF -> manySphere,
-volumeRender_kernel.cu:222).  One "step" = one frame rendered to device memory.
+volumeRender_kernel.cu:222).  One "step" = one frame of that workload rendered to
+device memory (and, for N > 1, gathered to rank 0 and assembled).
 
     python bench.py [--gpus N --steps K --warmup W]
-N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt in 8-row
-bands round-robin (nr_render_shard), each rank renders its bands, one RCCL gather
-(torch.distributed.gather over the "nccl" backend) brings them to rank 0, which
-re-interleaves them (nr_assemble_shards).  The frame size is fixed as N grows:
-scaling "strong".
+The K frames of the timed region go through nr_render_batch: the persistent tracer's
+pixel queue runs through the frames in order (up to 32 per launch), so one frame's
+longest rays march while the next frame's pixels keep the matrix cores busy -- every
+frame is rendered in full, none is reused.  config.single_frame repeats the timing with
+one nr_render call per frame (each launch waits for the previous frame's last ray).
+
+N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt in 8-row bands
+round-robin (nr_render_batch's shard arguments), each rank renders its bands of every
+frame, then one RCCL gather per frame (torch.distributed.gather over the "nccl" backend)
+brings them to rank 0, which re-interleaves them (nr_assemble_shards).  The frame size
+is fixed as N grows: scaling "strong".
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
 k_trace, f32 MFMA bound, per-launch HIP events on the stream it runs on) and
-`cpu_baseline` (the C oracle on the host cores, N = 1 only).  `value` is measured with
-one frame at a time; config.pipelined repeats the timing with --inflight frames in
-flight on separate streams (frame k+1's bulk fills the SIMDs frame k's tail leaves idle).
+`cpu_baseline` (the C oracle on the host cores, N = 1 only).
 """
 import argparse
 import json
@@ -31,24 +36,23 @@ sys.path.insert(0, REPO)
 
 FLOP_PER_EVAL = 2 * (3 * 32 + 7 * 32 * 32 + 32 * 1)   # 14,592
 PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}  # TFLOP/s dense, MI355X_MICROARCH.md
-W = H = 1024
 MAX_STEPS = 128
 BAND = 8
+MAX_BATCH = 32  # frames per k_trace launch (NR_MAX_BATCH)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
     ap.add_argument("--size", type=int, default=1024)
     ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
     ap.add_argument("--geometry", default="plane_1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-frame", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="frames in flight for the pipelined figure (config.pipelined); 1 = off")
     return ap.parse_args()
 
 
@@ -96,36 +100,43 @@ def main():
     size = a.size
     matcap = nr.load_png(nr.matcap_path("Chrome"))
     iv, nm = nr.camera(0.0, 0.0, 2.0)
-
     rows = nr.shard_rows(size, BAND, world, rank)
     max_rows = max(nr.shard_rows(size, BAND, world, s) for s in range(world))
 
-    class Slot:
-        """One frame in flight: a renderer context on its own stream + its buffers."""
+    stream = torch.cuda.Stream()
+    r = nr.Renderer(local)
+    r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
+    r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
+    r.set_stream(stream.cuda_stream)
 
-        def __init__(self):
-            self.stream = torch.cuda.Stream()
-            self.r = nr.Renderer(local)
-            self.r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
-            self.r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
-            self.r.set_stream(self.stream.cuda_stream)
-            self.shard = torch.zeros(max_rows * size, dtype=torch.int32, device="cuda")
-            self.gather = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if rank == 0 else None
-            self.frame = torch.zeros(size * size, dtype=torch.int32, device="cuda") if rank == 0 else None
+    nbuf = max(a.steps, a.warmup, 1)
+    shards = torch.zeros(nbuf, max_rows * size, dtype=torch.int32, device="cuda")
+    frames = shards if world == 1 else (
+        torch.zeros(nbuf, size * size, dtype=torch.int32, device="cuda") if rank == 0 else None)
+    gather = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if (rank == 0 and world > 1) else None
 
-        def step(self):
-            with torch.cuda.stream(self.stream):
-                if world == 1:
-                    self.r.render_device(self.frame.data_ptr(), size, size, a.max_steps)
-                    return
-                self.r.render_shard_device(self.shard.data_ptr(), size, size, BAND, world, rank, a.max_steps)
-                dist.gather(self.shard, list(self.gather.unbind(0)) if rank == 0 else None, dst=0)
-                if rank == 0:
-                    self.r.assemble_device(self.gather.data_ptr(), max_rows * size, self.frame.data_ptr(), size, size,
-                                           BAND, world)
+    def collect(i):
+        """Frame i's shards to rank 0: one RCCL gather + the re-interleave kernel."""
+        if world == 1:
+            return
+        dist.gather(shards[i], list(gather.unbind(0)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            r.assemble_device(gather.data_ptr(), max_rows * size, frames[i].data_ptr(), size, size, BAND, world)
 
-    slots = [Slot() for _ in range(max(1, a.inflight))]
-    r = slots[0].r
+    def run_batched(n):
+        if n == 0:
+            return
+        with torch.cuda.stream(stream):
+            r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size, [(iv, nm, 0)] * n,
+                                  a.max_steps, BAND, world, rank)
+            for i in range(n):
+                collect(i)
+
+    def run_single(n):
+        with torch.cuda.stream(stream):
+            for i in range(n):
+                r.render_shard_device(shards[i].data_ptr(), size, size, BAND, world, rank, a.max_steps)
+                collect(i)
 
     # work per frame (deterministic): ray-steps of this rank's shard, summed over ranks
     st = r.render_shard(size, size, BAND, world, rank, a.max_steps)[1]
@@ -134,55 +145,49 @@ def main():
         dist.all_reduce(steps_t)
     ray_steps, shade_evals = (float(v) for v in steps_t.tolist())
 
-    def timed(nslots, profile):
-        for i in range(a.warmup):
-            slots[i % nslots].step()
+    def timed(fn, profile):
+        fn(a.warmup)
         torch.cuda.synchronize()
-        for sl in slots[:nslots]:
-            sl.r.prof_collect()          # drop anything recorded so far
-            sl.r.set_profiling(profile)
+        r.prof_collect()          # drop anything recorded so far
+        r.set_profiling(profile)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for i in range(a.steps):
-            slots[i % nslots].step()
+        fn(a.steps)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        profs = []
-        for sl in slots[:nslots]:
-            sl.r.set_profiling(False)
-            profs.append(sl.r.prof_collect())
+        r.set_profiling(False)
+        prof = r.prof_collect()
         dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         if world > 1:
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        return float(dt_t.item()), profs
+        return float(dt_t.item()), prof
 
-    # headline: one frame at a time (each frame's launch starts after the previous one)
-    dt, profs = timed(1, True)
-    prof = profs[0]
-    # pipelined: `inflight` frames in flight on separate streams (frame k+1 fills the
-    # SIMDs that frame k's tail leaves idle)
-    dt_pipe = None
-    if a.inflight > 1:
-        dt_pipe, _ = timed(a.inflight, False)
-    frame = slots[(a.steps - 1) % (a.inflight if a.inflight > 1 else 1)].frame
+    dt, prof = timed(run_batched, True)
+    last = frames[a.steps - 1] if frames is not None else None
 
-    # parity spot-check of the timed output (outside the timed region)
+    # parity spot-check of the last timed frame (outside the timed region)
     parity = None
     if rank == 0:
         ref = r.render(size, size, a.max_steps, with_stats=False)
-        got = frame.cpu().numpy().view(np.uint32).reshape(size, size)
+        torch.cuda.synchronize()
+        got = last.cpu().numpy().view(np.uint32)[: size * size].reshape(size, size)
         parity = bool(np.array_equal(ref, got))
 
+    dt_single = None
+    if not a.no_single_frame:
+        dt_single, _ = timed(run_single, False)
+
     # roofline of the dominant kernel (k_trace) from this rank's per-launch events
-    march_avg_ms = prof["march_ms"] / max(prof["march_launches"], 1)
+    launches = max(prof["march_launches"], 1)
+    march_avg_ms = prof["march_ms"] / launches
     # k_trace evaluates the MLP for every march step AND the 4 tetrahedral samples of
     # every coloured ray (in-kernel shading), 14,592 algorithmic FLOP each
     local_evals = (st["ray_steps"] + st["shade_evals"]) * prof["renders"]
-    flop_per_launch = local_evals * FLOP_PER_EVAL / max(prof["march_launches"], 1)
+    flop_per_launch = local_evals * FLOP_PER_EVAL / launches
     achieved = flop_per_launch / (march_avg_ms * 1e-3) / 1e12 if march_avg_ms > 0 else 0.0
     peak = PEAK[a.precision]
 
@@ -192,7 +197,8 @@ def main():
     traffic = None
     try:
         tp = json.load(open(os.path.join(REPO, "profiles", "r1_pmc_traffic.json")))
-        if a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1:
+        if (a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1
+                and tp.get("frames_per_launch") == min(a.steps, MAX_BATCH)):
             traffic = tp["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         traffic = None
@@ -221,18 +227,21 @@ def main():
             "fps": round(a.steps / dt, 3),
             "ray_steps_per_frame": int(ray_steps),
             "shade_evals_per_frame": int(shade_evals),
-            "parallelism": f"row-band shards x{world} + RCCL gather" if world > 1 else "single GPU",
+            "frames_per_launch": min(a.steps, MAX_BATCH),
+            "schedule": "nr_render_batch: the K timed frames through one frame-major pixel queue "
+                        "(every frame rendered in full)",
+            "parallelism": f"row-band shards x{world} + one RCCL gather per frame" if world > 1 else "single GPU",
             "parity_vs_single_gpu_render": parity,
-            "pipelined": None if dt_pipe is None else {
-                "frames_in_flight": a.inflight,
-                "value": round(ray_steps * a.steps / dt_pipe / 1e6, 3),
-                "ms_per_step": round(dt_pipe / a.steps * 1e3, 4),
-                "fps": round(a.steps / dt_pipe, 3),
+            "single_frame": None if dt_single is None else {
+                "value": round(ray_steps * a.steps / dt_single / 1e6, 3),
+                "ms_per_step": round(dt_single / a.steps * 1e3, 4),
+                "fps": round(a.steps / dt_single, 3),
+                "schedule": "one nr_render_shard launch per frame",
             },
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "k_trace",
+            "kernel": "k_trace (batched instance)",
             "achieved": round(achieved, 3),
             "peak": peak,
             "unit": "TFLOP/s",
@@ -242,8 +251,8 @@ def main():
             "flop_per_launch": round(flop_per_launch, 1),
             "avg_launch_ms": round(march_avg_ms, 5),
             "launches": int(prof["march_launches"]),
-            "flop_basis": "(ray-steps + shade evals) x 14,592 FLOP per launch / mean k_trace duration "
-                          "(per-launch HIP events on the context stream)",
+            "flop_basis": "(ray-steps + shade evals) x 14,592 FLOP per frame x frames per launch / mean k_trace "
+                          "launch duration (per-launch HIP events on the context stream)",
         },
         "cpu_baseline": None,
     }

@@ -525,7 +525,6 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     T.take = c->wave_rays;
     T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
     const int cus = num_cus(c->device);
-    const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
     HIPCHK(c, hipEventRecord(c->ev0, s));
     int launches = 0;
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
@@ -534,6 +533,10 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         T.nframes = n;
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
+        // 3 workgroups (12 waves) per CU once several frames share the launch: the third
+        // wave per SIMD lifts the bulk rate, and the frames' tails overlap instead of
+        // adding up (tools/batch_bench.py); a lone frame keeps the single-frame default
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (n >= 4 ? 3 : 2);
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         int rc2;

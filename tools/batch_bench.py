@@ -1,0 +1,40 @@
+"""Per-GPU frame time of nr_render_batch on the bench frame (1024^2 plane_1, 128 steps,
+fp32, default camera) for 1/2/4/8 row-band shards and several batch sizes -- what one
+rank of the N-GPU bench sustains, without the gather.  Runs on the GPU box."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import cudaneuralrender_amd as nr  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--frames", type=int, default=64)
+ap.add_argument("--batches", default="1,4,16,32")
+ap.add_argument("--bpc", type=int, default=0)
+ap.add_argument("--rays", type=int, default=64)
+a = ap.parse_args()
+matcap = nr.load_png(nr.matcap_path("Chrome"))
+iv, nm = nr.camera(0, 0, 2)
+r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
+r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
+r.set_occupancy(a.bpc).set_wave_rays(a.rays)
+bufs = [torch.zeros(1024 * 1024, dtype=torch.int32, device="cuda") for _ in range(32)]
+for n in (1, 2, 4, 8):
+    line = []
+    for b in (int(x) for x in a.batches.split(",")):
+        cams = [(iv, nm, 0)] * b
+        ptrs = [t.data_ptr() for t in bufs[:b]]
+        for _ in range(2):
+            r.render_batch_device(ptrs, 1024, 1024, cams, 128, 8, n, 0)
+        r.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(max(1, a.frames // b)):
+            r.render_batch_device(ptrs, 1024, 1024, cams, 128, 8, n, 0)
+        r.synchronize()
+        dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
+        line.append(f"batch {b}: {dt:.3f} ms/frame")
+    print(f"n={n} bpc {a.bpc} rays {a.rays}: " + "  ".join(line), flush=True)

@@ -10,13 +10,15 @@ import json
 import sys
 
 out = sys.argv[1]
+batch = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+kname = "k_trace<0, false, false, true>" if batch else "k_trace<0, false, false, false>"
 
 
 def per_dispatch(counter_dir, name):
     vals = []
     for f in glob.glob(f"{counter_dir}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_trace<0, false, false>" in r["Kernel_Name"] and r["Counter_Name"] == name:
+            if kname in r["Kernel_Name"] and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals), len(vals)
 
@@ -25,14 +27,16 @@ fetch, nf = per_dispatch(f"{out}/fetch", "FETCH_SIZE")
 write, nw = per_dispatch(f"{out}/write", "WRITE_SIZE")
 hbm = fetch * 1024 * 2 + write * 1024
 print(json.dumps({
-    "kernel": "k_trace<0, false, false> (fp32)",
+    "kernel": kname + " (fp32)",
+    "frames_per_launch": batch if batch else 1,
     "workload": "plane_1 1024x1024, 128 march steps, fp32, Chrome.png, v1 scene, default camera",
-    "collection": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, tools/render_frames.py --frames 3",
+    "collection": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes, tools/render_frames.py "
+                  f"--frames 3 --batch {batch}",
     "dispatches": [nf, nw],
     "fetch_size_kb": round(fetch, 2),
     "write_size_kb": round(write, 2),
     "correction": "bytes = FETCH_SIZE*1024*2 (gfx950 under-reports wide reads 2x) + WRITE_SIZE*1024",
     "hbm_bytes_per_launch": int(hbm),
-    "algorithmic_bytes_per_launch": 1024 * 1024 * 4 + 30 * 1024 + 1024 * 1024,
+    "algorithmic_bytes_per_launch": (1024 * 1024 * 4) * max(batch, 1) + 30 * 1024 + 1024 * 1024,
     "note": "output pixels are written 4 B at a time as rays finish (scattered), hence write > 4 MiB",
 }, indent=1))
