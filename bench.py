@@ -15,8 +15,9 @@ one nr_render call per frame (each launch waits for the previous frame's last ra
 
 N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt in 8-row bands
 round-robin (nr_render_batch's shard arguments), each rank renders its bands of every
-frame, then one RCCL gather per frame (torch.distributed.gather over the "nccl" backend)
-brings them to rank 0, which re-interleaves them (nr_assemble_shards).  The frame size
+frame, then one RCCL gather (torch.distributed.gather over the "nccl" backend) brings
+the batch's shards to rank 0 -- one collective for the K frames, single-frame timing:
+one per frame -- which re-interleaves each frame (nr_assemble_shards).  The frame size
 is fixed as N grows: scaling "strong".
 
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
@@ -110,18 +111,23 @@ def main():
     r.set_stream(stream.cuda_stream)
 
     nbuf = max(a.steps, a.warmup, 1)
-    shards = torch.zeros(nbuf, max_rows * size, dtype=torch.int32, device="cuda")
+    shard_px = max_rows * size
+    shards = torch.zeros(nbuf, shard_px, dtype=torch.int32, device="cuda")
     frames = shards if world == 1 else (
         torch.zeros(nbuf, size * size, dtype=torch.int32, device="cuda") if rank == 0 else None)
-    gather = torch.zeros(world, max_rows * size, dtype=torch.int32, device="cuda") if (rank == 0 and world > 1) else None
+    gather = torch.zeros(world, nbuf * shard_px, dtype=torch.int32, device="cuda") if (rank == 0 and world > 1) else None
 
-    def collect(i):
-        """Frame i's shards to rank 0: one RCCL gather + the re-interleave kernel."""
+    def collect(i0, n):
+        """Frames i0..i0+n-1 to rank 0: ONE RCCL gather of the n shards of every rank, then
+        the re-interleave kernel per frame (rank s's shard of frame i at gather[s][i])."""
         if world == 1:
             return
-        dist.gather(shards[i], list(gather.unbind(0)) if rank == 0 else None, dst=0)
+        src = shards[i0:i0 + n].reshape(-1)
+        dist.gather(src, [g[: n * shard_px] for g in gather.unbind(0)] if rank == 0 else None, dst=0)
         if rank == 0:
-            r.assemble_device(gather.data_ptr(), max_rows * size, frames[i].data_ptr(), size, size, BAND, world)
+            for i in range(n):
+                r.assemble_device(gather.data_ptr() + i * shard_px * 4, nbuf * shard_px, frames[i0 + i].data_ptr(),
+                                  size, size, BAND, world)
 
     def run_batched(n):
         if n == 0:
@@ -129,14 +135,13 @@ def main():
         with torch.cuda.stream(stream):
             r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size, [(iv, nm, 0)] * n,
                                   a.max_steps, BAND, world, rank)
-            for i in range(n):
-                collect(i)
+            collect(0, n)
 
     def run_single(n):
         with torch.cuda.stream(stream):
             for i in range(n):
                 r.render_shard_device(shards[i].data_ptr(), size, size, BAND, world, rank, a.max_steps)
-                collect(i)
+                collect(i, 1)
 
     # work per frame (deterministic): ray-steps of this rank's shard, summed over ranks
     st = r.render_shard(size, size, BAND, world, rank, a.max_steps)[1]
@@ -230,7 +235,8 @@ def main():
             "frames_per_launch": min(a.steps, MAX_BATCH),
             "schedule": "nr_render_batch: the K timed frames through one frame-major pixel queue "
                         "(every frame rendered in full)",
-            "parallelism": f"row-band shards x{world} + one RCCL gather per frame" if world > 1 else "single GPU",
+            "parallelism": f"row-band shards x{world} + one RCCL gather per batch of frames" if world > 1
+                           else "single GPU",
             "parity_vs_single_gpu_render": parity,
             "single_frame": None if dt_single is None else {
                 "value": round(ray_steps * a.steps / dt_single / 1e6, 3),
