@@ -126,13 +126,43 @@ __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0
 // in a single instruction, bias preloaded as the accumulator); layer 0 on the f32
 // matrix core as in the fp32 path; final layer in fp32 on VALU.  Register k = 4mt + r
 // of group g holds unit 16mt + 4g + r (the MFMA C layout, unpermuted).
+// bias + ReLU of one tile's two accumulators straight into the packed 16-bit B operand
+// of the next layer: v_cvt_pk_{bf16,f16}_f32 rounds pairs (RNE), v_pk_max_i16 against 0
+// is the ReLU on the 16-bit patterns (negative values and -0 have the sign bit set) --
+// 8 VALU per tile instead of 8 fmaxf + 4 conversions.
+template <int PREC>
+__device__ __forceinline__ void relu_pack(const f32x4 &c0, const f32x4 &c1, uint32_t ap[4]) {
+    typedef typename std::conditional<PREC == NR_PRECISION_BF16, __bf16, _Float16>::type e16;
+    typedef e16 e16x2 __attribute__((ext_vector_type(2)));
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const f32x2 v[4] = {{c0[0], c0[1]}, {c0[2], c0[3]}, {c1[0], c1[1]}, {c1[2], c1[3]}};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const s16x2 h = __builtin_bit_cast(s16x2, __builtin_convertvector(v[q], e16x2));
+        ap[q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (s16x2){0, 0}));
+    }
+}
+
+template <int PREC>
+__device__ __forceinline__ f32x4 mfma_lowp(const void *w, const uint32_t ap[4], const f32x4 &cinit) {
+    typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const v8 b = __builtin_bit_cast(v8, (u32x4){ap[0], ap[1], ap[2], ap[3]});
+    if constexpr (PREC == NR_PRECISION_BF16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const v8 *>(w), b, cinit, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(*reinterpret_cast<const v8 *>(w), b, cinit, 0, 0, 0);
+}
+
 template <int PREC, int NT>
 __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh, float fr, float x, float y, float z) {
     typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
-    typedef typename std::conditional<PREC == NR_PRECISION_BF16, __bf16, _Float16>::type e16;
     const int lane = lane_id(), g = lane >> 4, j = lane & 15;
-    float a[NT][8];
+    uint32_t ap[NT][4];  // activations of the hidden layers, packed 16-bit B operands
+    float a[NT][8];      // fp32 activations feeding the final layer
+    f32x4 c0[NT], c1[NT];
     {
         const float w0 = fl[lane], w1 = fl[64 + lane];
         const float4 *bb = reinterpret_cast<const float4 *>(fl + 128 + g * 8);
@@ -142,16 +172,14 @@ __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, 
             const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
             const float pw = in0 == 4 ? __shfl(fr, 16 * t + j) : 0.0f;
             const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : pw));
-            const f32x4 c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{blo.x, blo.y, blo.z, blo.w}, 0, 0, 0);
-            const f32x4 c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{bhi.x, bhi.y, bhi.z, bhi.w}, 0, 0, 0);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                a[t][r] = fmaxf(c0[r], 0.0f);
-                a[t][4 + r] = fmaxf(c1[r], 0.0f);
-            }
+            c0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{blo.x, blo.y, blo.z, blo.w}, 0, 0, 0);
+            c1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{bhi.x, bhi.y, bhi.z, bhi.w}, 0, 0, 0);
         }
     }
+    // hidden layers; the last one's output stays fp32 for the final layer
     for (int jl = 0; jl < nh; ++jl) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) relu_pack<PREC>(c0[t], c1[t], ap[t]);
         const v8 *A = reinterpret_cast<const v8 *>(lp + (size_t)jl * LP_A_ELEMS);
         const v8 w0 = A[lane], w1 = A[64 + lane];
         const float4 *bb = reinterpret_cast<const float4 *>(fl + 160 + 32 * jl + g * 8);
@@ -159,24 +187,17 @@ __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, 
         const f32x4 c0i = {blo.x, blo.y, blo.z, blo.w}, c1i = {bhi.x, bhi.y, bhi.z, bhi.w};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            v8 b;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) b[e] = (e16)a[t][e];
-            f32x4 c0, c1;
-            if constexpr (PREC == NR_PRECISION_BF16) {
-                c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, b, c0i, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, b, c1i, 0, 0, 0);
-            } else {
-                c0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, b, c0i, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, b, c1i, 0, 0, 0);
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                a[t][r] = fmaxf(c0[r], 0.0f);
-                a[t][4 + r] = fmaxf(c1[r], 0.0f);
-            }
+            c0[t] = mfma_lowp<PREC>(&w0, ap[t], c0i);
+            c1[t] = mfma_lowp<PREC>(&w1, ap[t], c1i);
         }
     }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            a[t][r] = fmaxf(c0[t][r], 0.0f);
+            a[t][4 + r] = fmaxf(c1[t][r], 0.0f);
+        }
     const float *wf = fl + 160 + 32 * nh + g * 8;
     const float bf = fl[160 + 32 * nh + 32];
     float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
