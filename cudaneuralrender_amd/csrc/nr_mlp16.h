@@ -177,9 +177,8 @@ __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, 
         }
     }
     // hidden layers; the last one's output stays fp32 for the final layer
+    // (tile t's pack is issued right before its MFMAs, so it overlaps tile t-1's)
     for (int jl = 0; jl < nh; ++jl) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t) relu_pack<PREC>(c0[t], c1[t], ap[t]);
         const v8 *A = reinterpret_cast<const v8 *>(lp + (size_t)jl * LP_A_ELEMS);
         const v8 w0 = A[lane], w1 = A[64 + lane];
         const float4 *bb = reinterpret_cast<const float4 *>(fl + 160 + 32 * jl + g * 8);
@@ -187,6 +186,7 @@ __device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, 
         const f32x4 c0i = {blo.x, blo.y, blo.z, blo.w}, c1i = {bhi.x, bhi.y, bhi.z, bhi.w};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
+            relu_pack<PREC>(c0[t], c1[t], ap[t]);
             c0[t] = mfma_lowp<PREC>(&w0, ap[t], c0i);
             c1[t] = mfma_lowp<PREC>(&w1, ap[t], c1i);
         }
