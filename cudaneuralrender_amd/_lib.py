@@ -15,7 +15,7 @@ NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}
 NR_SCENE = {"v1": 0, "tanh": 1}
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
-NR_SCHEDULE = {"persistent": 0, "wavefront": 1}
+NR_SCHEDULE = {"persistent": 0, "wavefront": 1, "layered": 2}
 
 # every symbol include/neural_render.h declares
 EXPORTS = [
@@ -25,7 +25,7 @@ EXPORTS = [
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
-    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards",
+    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk",
 ]
 
 
@@ -128,6 +128,7 @@ def lib():
         "nr_set_cost_probe": (I, [P, I, I]),
         "nr_set_wave_rays": (I, [P, I]),
         "nr_set_queue_shards": (I, [P, I]),
+        "nr_set_layer_chunk": (I, [P, ctypes.c_long]),
         "nr_set_temporal_order": (I, [P, I]),
         "nr_dense_forward": (I, [P, P, P, I, I, I, P, P, L64, I]),
         "nr_debug_stamps": (I, [P, P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),

@@ -89,6 +89,15 @@ struct nr_ctx {
     size_t cap_io = 0;
     float *d_io = nullptr;           // mlp_forward staging
     int check_every = 32;            // host polls the live count every N iterations
+    // layered schedule (any dense network): per-frame args in device memory, the frame's
+    // launch sequence captured once per image configuration and replayed as a hipGraph
+    RenderArgs *d_rargs = nullptr;
+    float *d_lsdf = nullptr, *d_lz = nullptr;  // SDFs (4 per converged ray), layer scratch
+    size_t cap_lsdf = 0, cap_lz = 0;
+    hipGraphExec_t lgraph = nullptr;
+    std::vector<long long> lkey;               // configuration lgraph was captured for
+    long long net_ver = 0;                     // bumped by every network upload
+    long layer_chunk = 0;                      // nr_set_layer_chunk (0: auto)
 
     // per-launch profiling (nr_set_profiling)
     bool profiling = false;
@@ -130,6 +139,9 @@ int free_network(nr_ctx *c) {
     dfree(c->d_pack32); dfree(c->d_lp); dfree(c->d_lpf);
     dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16);
     c->fused = false;
+    if (c->lgraph) { (void)hipGraphExecDestroy(c->lgraph); c->lgraph = nullptr; }
+    c->lkey.clear();
+    ++c->net_ver;
     return NR_OK;
 }
 
@@ -269,6 +281,156 @@ int num_cus(int dev) {
     return cus;
 }
 
+
+// one dense layer over n rows (k_dense<0>)
+hipError_t dense_rows(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
+                      int cus, hipStream_t s) {
+    DenseArgs D{};
+    D.W = W; D.b = b; D.A = A; D.Z = Z;
+    D.n = n; D.chunk0 = 0; D.chunk_n = n;
+    D.in = in; D.out = out; D.relu = relu;
+    const int grid = (int)std::max<long>(1, std::min<long>((n * out + 255) / 256, (long)cus * 8));
+    return launch_dense(D, 0, grid, s);
+}
+
+// stats of the queue schedules (wavefront, layered) from their per-iteration counters
+int queue_stats(nr_ctx *c, int max_steps, int launches, nr_stats *stats, hipStream_t s) {
+    if (!stats) return NR_OK;
+    const size_t nctr = (size_t)2 * max_steps + 2;
+    HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_ctr, nctr * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    nr_stats st{};
+    uint64_t steps = 0;
+    int iters = 0;
+    for (int it = 0; it < max_steps; ++it) {
+        steps += c->h_ctr[it];
+        if (c->h_ctr[it]) iters = std::max(iters, it + 1);
+        if (c->h_ctr[max_steps + 2 + it]) iters = std::max(iters, std::min(it + 2, max_steps));
+    }
+    st.ray_steps = steps;
+    st.rays_hit = c->h_ctr[0];
+    st.rays_shaded = c->h_ctr[max_steps + 1];
+    st.shade_evals = 4ull * st.rays_shaded;
+    st.iterations = iters;
+    st.launches = launches;
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    st.ms_total = ms;
+    *stats = st;
+    return NR_OK;
+}
+
+// Layered schedule: the reference's structure (render_kernel :608-692, one
+// NeuralNetwork::forward over the live points per iteration, denseLayer.cu:229-278) for
+// any dense [3|4, ..., 1] network.  Per iteration: the dense layers over the live-ray
+// queue in chunks of lchunk points (bounded scratch, the kernel.cu:659-660 TODO), then
+// k_march_l; at the end the layers over 4 points per converged ray and k_shade_l.  All
+// counts stay on the device; the whole frame is captured once per configuration and
+// replayed as a hipGraph (the per-frame RenderArgs are rewritten in device memory by
+// k_set_args before each replay).  fp32 throughout (nr_set_precision applies to the
+// fused kernels).
+int render_layered(nr_ctx *c, const RenderArgs &A0, uint32_t *out, size_t npix, int max_steps, int loc, nr_stats *stats,
+                   hipStream_t s) {
+    const int nl = (int)c->dims.size() - 1;
+    if (c->dims[0] > 4) return set_err(c, NR_E_FORMAT, "nr_render: at most 4 network inputs (has %d)", c->dims[0]);
+    int maxw = 1;
+    for (int l = 1; l < nl; ++l) maxw = std::max(maxw, c->dims[l]);
+    // chunk: 128 MiB per scratch buffer, at least 64K points, at most what a frame needs
+    const long lchunk = c->layer_chunk > 0 ? c->layer_chunk
+                                           : std::min<long>(4l * (long)npix, std::max<long>(65536, (128l << 20) / (4l * maxw)));
+    int rc;
+    if ((rc = ensure_rays(c, npix)) != NR_OK) return rc;
+    if ((rc = ensure_ctr(c, (size_t)2 * max_steps + 8)) != NR_OK) return rc;
+    if ((rc = ensure_buf(c, c->d_lsdf, c->cap_lsdf, 4 * npix)) != NR_OK) return rc;
+    if ((rc = ensure_buf(c, c->d_lz, c->cap_lz, (size_t)2 * lchunk * maxw)) != NR_OK) return rc;
+    if (!c->d_rargs) HIPCHK(c, hipMalloc(&c->d_rargs, sizeof(RenderArgs)));
+    RenderArgs A = A0;
+    if (loc != NR_DEVICE) {
+        if ((rc = ensure_buf(c, c->d_out, c->cap_out, npix)) != NR_OK) return rc;
+        A.out = c->d_out;
+    }
+    const int cus = num_cus(c->device);
+    const int step_grid = (int)std::max<size_t>(1, std::min<size_t>((npix + 255) / 256, (size_t)cus * 4));
+    const int shade_grid = (int)std::max<size_t>(1, std::min<size_t>((npix + 1023) / 1024, (size_t)cus * 4));
+    const long nch_march = ((long)npix + lchunk - 1) / lchunk, nch_shade = (4l * (long)npix + lchunk - 1) / lchunk;
+    uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + max_steps + 1, *shade_it = c->d_ctr + max_steps + 2;
+    const size_t nctr = (size_t)2 * max_steps + 2;
+    float *zb[2] = {c->d_lz, c->d_lz + (size_t)lchunk * maxw};
+    QueueArgs Q{};
+    Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
+    // the dense chain over one chunk of a queue (src 1: live rays, 2: tetrahedron points)
+    auto chain = [&](int src, const float4 *pts, const uint32_t *count, int mul, long chunk0) -> hipError_t {
+        for (int l = 0; l < nl; ++l) {
+            DenseArgs D{};
+            D.W = c->d_W[l]; D.b = c->d_b[l];
+            D.in = c->dims[l]; D.out = c->dims[l + 1]; D.relu = l != nl - 1;
+            D.A = l == 0 ? nullptr : zb[(l - 1) & 1];
+            D.Z = l == nl - 1 ? c->d_lsdf + chunk0 : zb[l & 1];
+            D.pts = pts; D.count = count; D.count_mul = mul; D.args = c->d_rargs;
+            D.chunk0 = chunk0; D.chunk_n = lchunk;
+            const int grid = (int)std::max<long>(1, std::min<long>((lchunk * D.out + 255) / 256, (long)cus * 8));
+            hipError_t e = launch_dense(D, l == 0 ? src : 0, grid, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    // one frame's launches (captured into the graph, or issued directly for long caps)
+    auto frame = [&]() -> hipError_t {
+        hipError_t e = hipMemsetAsync(c->d_ctr, 0, nctr * 4, s);
+        if (e != hipSuccess) return e;
+        Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
+        if ((e = launch_init_l(c->d_rargs, Q, (long)npix, s)) != hipSuccess) return e;
+        for (int it = 0; it < max_steps; ++it) {
+            Q.cnt_in = cnt + it; Q.cnt_out = cnt + it + 1;
+            Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
+            Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
+            for (long ch = 0; ch < nch_march; ++ch)
+                if ((e = chain(1, Q.p_in, Q.cnt_in, 1, ch * lchunk)) != hipSuccess) return e;
+            if ((e = launch_march_l(c->d_rargs, Q, c->d_lsdf, it, step_grid, s)) != hipSuccess) return e;
+        }
+        for (long ch = 0; ch < nch_shade; ++ch)
+            if ((e = chain(2, c->d_SP, shade_cnt, 4, ch * lchunk)) != hipSuccess) return e;
+        return launch_shade_l(c->d_rargs, Q, c->d_lsdf, shade_grid, s);
+    };
+    const int launches = 2 + max_steps * (int)(1 + nch_march * nl) + (int)(nch_shade * nl) + 1;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, launch_set_args(A, c->d_rargs, s));
+    if ((rc = prof_begin(c, 1, s)) != NR_OK) return rc;
+    // graph unless: long caps, the legacy null stream (not capturable), or debug bit 256
+    // (direct launches, for profilers that do not follow graph launches)
+    if (max_steps <= 1024 && s != nullptr && !(c->debug & 256)) {
+        const std::vector<long long> key = {A.W, A.rows, A.band, A.nshards, A.shard, max_steps, c->net_ver, lchunk,
+                                            (long long)(uintptr_t)c->d_P[0], (long long)(uintptr_t)c->d_ctr,
+                                            (long long)(uintptr_t)c->d_lsdf, (long long)(uintptr_t)c->d_lz,
+                                            (long long)(uintptr_t)c->d_SP, (long long)(uintptr_t)s};
+        if (!c->lgraph || key != c->lkey) {
+            if (c->lgraph) { HIPCHK(c, hipGraphExecDestroy(c->lgraph)); c->lgraph = nullptr; }
+            hipGraph_t g = nullptr;
+            HIPCHK(c, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+            hipError_t e = frame();
+            hipError_t e2 = hipStreamEndCapture(s, &g);
+            if (e != hipSuccess || e2 != hipSuccess) {
+                if (g) (void)hipGraphDestroy(g);
+                return set_err(c, NR_E_HIP, "nr_render: layered graph capture failed: %s",
+                               hipGetErrorString(e != hipSuccess ? e : e2));
+            }
+            e = hipGraphInstantiate(&c->lgraph, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            if (e != hipSuccess) { c->lgraph = nullptr; return set_err(c, NR_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e)); }
+            c->lkey = key;
+        }
+        HIPCHK(c, hipGraphLaunch(c->lgraph, s));
+    } else {
+        HIPCHK(c, frame());
+    }
+    if ((rc = prof_end(c, s)) != NR_OK) return rc;
+    if (c->profiling) c->prof_renders++;
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, A.out, npix * 4, hipMemcpyDeviceToHost, s));
+    if (!stats && loc != NR_DEVICE) HIPCHK(c, hipStreamSynchronize(s));
+    return queue_stats(c, max_steps, launches, stats, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -323,6 +485,7 @@ int nr_destroy(nr_ctx *c) {
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
     dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -440,8 +603,9 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (W < 1 || H < 1 || (long)W * H > (1l << 31)) return set_err(c, NR_E_INVALID, "nr_render: bad size %dx%d", W, H);
     if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
     if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
-    if (c->schedule != NR_SCHED_PERSISTENT || (c->debug & (1 | 8))) {
-        // frame by frame (the wavefront schedule and the diagnostics are single-frame)
+    if (c->schedule != NR_SCHED_PERSISTENT || !c->fused || (c->debug & (1 | 8))) {
+        // frame by frame (the wavefront and layered schedules and the diagnostics are
+        // single-frame)
         float iv[12], nm[16];
         memcpy(iv, c->inv_view, sizeof iv);
         memcpy(nm, c->normal, sizeof nm);
@@ -588,9 +752,8 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
     if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
     if (c->dims.empty()) return set_err(c, NR_E_STATE, "nr_render: no network loaded");
-    if (!c->fused)
-        return set_err(c, NR_E_FORMAT, "nr_render: network shape unsupported by the fused march kernel "
-                                       "(needs [3|4, 32, ..., 32, 1])");
+    if (c->dims.back() != 1)
+        return set_err(c, NR_E_FORMAT, "nr_render: the SDF network must have one output (has %d)", c->dims.back());
     if (c->dims[0] != c->num_inputs)
         return set_err(c, NR_E_STATE, "nr_render: network takes %d inputs but numInputs = %d", c->dims[0], c->num_inputs);
     if (c->color_type == NR_COLOR_MATCAP && !c->d_matcap) return set_err(c, NR_E_STATE, "nr_render: matcap colouring without a matcap");
@@ -616,6 +779,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     GET_STREAM(c, s);
     int cus = num_cus(c->device);
     int rc2;
+    if (!c->fused || c->schedule == NR_SCHED_LAYERED) return render_layered(c, A, out, npix, max_steps, loc, stats, s);
     if (c->schedule == NR_SCHED_PERSISTENT) {
         // 8 shard counters on their own 128-byte lines, then 4 x u64 stats
         // (a second set for the cost probe)
@@ -757,30 +921,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     if (c->profiling) c->prof_renders++;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
-    if (stats) {
-        HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_ctr, nctr * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        uint64_t steps = 0;
-        int iters = 0;
-        for (int it = 0; it < max_steps; ++it) {
-            steps += c->h_ctr[it];
-            if (c->h_ctr[it]) iters = std::max(iters, it + 1);
-            if (c->h_ctr[max_steps + 2 + it]) iters = std::max(iters, std::min(it + 2, max_steps));
-        }
-        st.ray_steps = steps;
-        st.rays_hit = c->h_ctr[0];
-        st.rays_shaded = c->h_ctr[max_steps + 1];
-        st.shade_evals = 4ull * st.rays_shaded;
-        st.iterations = iters;
-        st.launches = launches;
-        float ms = 0;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        st.ms_total = ms;
-        *stats = st;
-    } else if (loc != NR_DEVICE) {
-        HIPCHK(c, hipStreamSynchronize(s));
-    }
-    return NR_OK;
+    return queue_stats(c, max_steps, launches, stats, s);
 }
 
 int nr_render(nr_ctx *c, uint32_t *out, int W, int H, int max_steps, int loc, nr_stats *stats) {
@@ -815,7 +956,9 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
     float *dY = Y;
     int rc;
     int maxw = *std::max_element(c->dims.begin(), c->dims.end());
-    size_t need = (loc == NR_DEVICE ? 0 : (size_t)n * (in0 + outn)) + (c->fused ? 0 : (size_t)2 * n * maxw);
+    // the generic chain runs in chunks of at most 64 MiB of activations per buffer
+    const long chunk = std::min<long>(n, std::max<long>(16384, (64l << 20) / (4l * maxw)));
+    size_t need = (loc == NR_DEVICE ? 0 : (size_t)n * (in0 + outn)) + (c->fused ? 0 : (size_t)2 * chunk * maxw);
     if ((rc = ensure_buf(c, c->d_io, c->cap_io, need)) != NR_OK) return rc;
     float *scratch = c->d_io;
     if (loc != NR_DEVICE) {
@@ -834,12 +977,16 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         else  // 32-point-tile variant (k_mlp), kept for comparison
             HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
     } else {
-        const float *a = dX;
-        float *bufs[2] = {scratch, scratch + (size_t)n * maxw};
-        for (int l = 0; l < nl; ++l) {
-            float *z = (l == nl - 1) ? dY : bufs[l & 1];
-            HIPCHK(c, launch_dense(c->d_W[l], c->d_b[l], a, z, n, c->dims[l], c->dims[l + 1], l != nl - 1, s));
-            a = z;
+        float *bufs[2] = {scratch, scratch + (size_t)chunk * maxw};
+        const int cus = num_cus(c->device);
+        for (long p0 = 0; p0 < n; p0 += chunk) {
+            const long m = std::min(chunk, n - p0);
+            const float *a = dX + (size_t)p0 * in0;
+            for (int l = 0; l < nl; ++l) {
+                float *z = (l == nl - 1) ? dY + (size_t)p0 * outn : bufs[l & 1];
+                HIPCHK(c, dense_rows(c->d_W[l], c->d_b[l], a, z, m, c->dims[l], c->dims[l + 1], l != nl - 1, cus, s));
+                a = z;
+            }
         }
     }
     if (loc != NR_DEVICE) {
@@ -867,7 +1014,7 @@ int nr_layer_forward(nr_ctx *c, int layer, const float *A, float *Z, long n, int
         HIPCHK(c, hipMemcpyAsync(ha, A, (size_t)n * in * 4, hipMemcpyHostToDevice, s));
         dA = ha;
     }
-    HIPCHK(c, launch_dense(c->d_W[layer], c->d_b[layer], dA, dZ, n, in, out, layer != nl - 1, s));
+    HIPCHK(c, dense_rows(c->d_W[layer], c->d_b[layer], dA, dZ, n, in, out, layer != nl - 1, num_cus(c->device), s));
     if (loc != NR_DEVICE) {
         HIPCHK(c, hipMemcpyAsync(Z, dZ, (size_t)n * out * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -905,7 +1052,7 @@ int nr_prof_collect(nr_ctx *c, nr_kernel_prof *out) {
 
 int nr_set_schedule(nr_ctx *c, int schedule) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    if (schedule != NR_SCHED_PERSISTENT && schedule != NR_SCHED_WAVEFRONT)
+    if (schedule != NR_SCHED_PERSISTENT && schedule != NR_SCHED_WAVEFRONT && schedule != NR_SCHED_LAYERED)
         return set_err(c, NR_E_INVALID, "unknown schedule %d", schedule);
     c->schedule = schedule;
     return NR_OK;
@@ -938,6 +1085,13 @@ int nr_set_cost_probe(nr_ctx *c, int max_steps, int rays_per_wave) {
     c->probe_steps = max_steps;
     c->probe_take = rays_per_wave;
     c->probe_dilate = (c->debug & 16) ? 0 : 1;
+    return NR_OK;
+}
+
+int nr_set_layer_chunk(nr_ctx *c, long points) {
+    if (!c || points < 0 || (points > 0 && points < 64))
+        return set_err(c, NR_E_INVALID, "nr_set_layer_chunk: points must be 0 (auto) or >= 64");
+    c->layer_chunk = points;
     return NR_OK;
 }
 
@@ -993,7 +1147,7 @@ int nr_dense_forward(nr_ctx *c, const float *W, const float *b, int in, int out,
     HIPCHK(c, hipSetDevice(c->device));
     GET_STREAM(c, s);
     if (loc == NR_DEVICE) {
-        HIPCHK(c, launch_dense(W, b, A, Z, n, in, out, relu, s));
+        HIPCHK(c, dense_rows(W, b, A, Z, n, in, out, relu, num_cus(c->device), s));
         return NR_OK;
     }
     // host buffers: stage everything
@@ -1004,7 +1158,7 @@ int nr_dense_forward(nr_ctx *c, const float *W, const float *b, int in, int out,
     HIPCHK(c, hipMemcpyAsync(dW, W, (size_t)in * out * 4, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(db, b, (size_t)out * 4, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(dA, A, (size_t)n * in * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_dense(dW, db, dA, dZ, n, in, out, relu, s));
+    HIPCHK(c, dense_rows(dW, db, dA, dZ, n, in, out, relu, num_cus(c->device), s));
     HIPCHK(c, hipMemcpyAsync(Z, dZ, (size_t)n * out * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     return NR_OK;

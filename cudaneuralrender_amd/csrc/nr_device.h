@@ -213,4 +213,43 @@ __device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t *counter) {
     return base + (uint32_t)__popcll(below);
 }
 
+// Block-aggregated append to two queues: one atomic per queue per block.  Same-address
+// atomics serialise at ~10 ns each in L2, so per-wave appends of a 1M-ray queue cost
+// more than the step itself.  Every thread of the block (<= 16 waves) must call it.
+struct Slots {
+    uint32_t a, b;    // this lane's slot in queue a / b (valid where its predicate holds)
+    uint32_t na, nb;  // the block's totals
+};
+__device__ __forceinline__ Slots block_append2(bool pa, uint32_t *ca, bool pb, uint32_t *cb) {
+    __shared__ uint32_t s_app[2][17];  // per-wave counts -> exclusive offsets; [16] = base, then total
+    __shared__ uint32_t s_tot[2];
+    const int wv = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6, lane = lane_id();
+    const uint64_t ma = __ballot(pa), mb = __ballot(pb);
+    if (lane == 0) {
+        s_app[0][wv] = (uint32_t)__popcll(ma);
+        s_app[1][wv] = (uint32_t)__popcll(mb);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int q = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < nw; ++w) {
+            const uint32_t c = s_app[q][w];
+            s_app[q][w] = tot;
+            tot += c;
+        }
+        s_app[q][16] = tot ? atomicAdd(q ? cb : ca, tot) : 0u;
+        s_tot[q] = tot;
+    }
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1ull;
+    Slots r;
+    r.a = s_app[0][16] + s_app[0][wv] + (uint32_t)__popcll(ma & below);
+    r.b = s_app[1][16] + s_app[1][wv] + (uint32_t)__popcll(mb & below);
+    r.na = s_tot[0];
+    r.nb = s_tot[1];
+    __syncthreads();  // the arrays are reused by the next call
+    return r;
+}
+
 }  // namespace nr

@@ -37,6 +37,19 @@ struct QueueArgs {
     uint32_t *shade_it;     // per-iteration count of waves that enqueued converged rays
 };
 
+// One dense layer over a chunk of points (k_dense; layered schedule and the generic
+// nr_mlp_forward).  Z is chunk-local [chunk][out].
+struct DenseArgs {
+    const float *W, *b;        // out-major [out][in], bias [out]
+    const float *A;            // SRC 0: chunk-local rows [chunk][in]
+    float *Z;
+    const float4 *pts;         // SRC 1: live-ray queue; SRC 2: converged-ray queue
+    const uint32_t *count;     // device-side point count (x count_mul), or NULL: use n
+    const RenderArgs *args;    // SRC 1/2: the frame number (4th input)
+    long n, chunk0, chunk_n;
+    int count_mul, in, out, relu, lds;
+};
+
 // Persistent-schedule state (nr_trace.hip).
 // One frame of a batched launch (nr_render_batch): its camera, sphere-grid offset,
 // animation input and output image.  Staged into LDS by k_trace<.., BATCH>.
@@ -78,8 +91,12 @@ struct TraceArgs {
 
 int smem_bytes(const MlpArgs &M, int prec);
 hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
-hipError_t launch_dense(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
-                        hipStream_t st);
+int dense_lds_bytes(int in, int out);
+hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
+hipError_t launch_set_args(const RenderArgs &A, RenderArgs *d, hipStream_t st);
+hipError_t launch_init_l(const RenderArgs *Ad, const QueueArgs &Q, long npix, hipStream_t st);
+hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf, int it, int grid, hipStream_t st);
+hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st);
 hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st);
 hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int prec, int it, int grid,
                         hipStream_t st);

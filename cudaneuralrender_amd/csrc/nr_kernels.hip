@@ -228,24 +228,291 @@ __global__ __launch_bounds__(256) void k_mlp(MlpArgs M, int prec, const float *_
 }
 
 // Generic dense layer, one thread per (point, output): DenseLayer::forward for any
-// shape (denseLayer.cu:229-278).  W out-major [out][in].
-__global__ void k_dense(const float *__restrict__ W, const float *__restrict__ b, const float *__restrict__ A,
-                        float *__restrict__ Z, long n, int in, int out, int relu) {
-    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * out) return;
-    long p = t / out;
-    int o = (int)(t - p * out);
-    const float *w = W + (long)o * in;
-    const float *a = A + p * in;
-    float acc = 0.0f;
-    for (int k = 0; k < in; ++k) acc = __builtin_fmaf(w[k], a[k], acc);
-    float v = acc + b[o];
-    if (relu) v = fmaxf(v, 0.0f);
-    Z[t] = v;
+// shape (denseLayer.cu:229-278).  W out-major [out][in], staged in LDS with rows padded
+// to in + 1 floats (lanes of a wave read consecutive rows) when it fits.  The point
+// count is D.n, or read from the device (D.count x D.count_mul) when the points are a
+// ray queue whose length the host does not know; the launch covers points
+// [chunk0, chunk0 + chunk_n) of it.  SRC: 0 = rows of D.A (chunk-local), 1 = the live
+// rays' positions (+ the frame number as a 4th input), 2 = the four tetrahedron points
+// of each converged ray (surfaceNormal, :361-377).  Arithmetic: ascending-k fmaf chain,
+// then + bias, then ReLU (the fused kernels' and the oracle's order).
+template <int SRC>
+__global__ __launch_bounds__(256) void k_dense(DenseArgs D) {
+    extern __shared__ float sw[];
+    const long n = D.count ? (long)(*D.count) * D.count_mul : D.n;
+    const long nc = min(n - D.chunk0, D.chunk_n);
+    if (nc <= 0) return;  // uniform over the block
+    const int in = D.in, out = D.out;
+    const float *W = D.W;
+    int ws = in;
+    if (D.lds) {
+        ws = in + 1;
+        for (int i = threadIdx.x; i < in * out; i += blockDim.x) sw[(i / in) * ws + i % in] = D.W[i];
+        __syncthreads();
+        W = sw;
+    }
+    float fr = 0.0f;
+    if constexpr (SRC != 0) fr = (float)D.args->frame;
+    const long tot = nc * out;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (long)gridDim.x * blockDim.x) {
+        const long p = t / out;
+        const int o = (int)(t - p * out);
+        const float *w = W + o * ws;
+        float acc = 0.0f;
+        if constexpr (SRC == 0) {
+            const float *a = D.A + p * in;
+            for (int k = 0; k < in; ++k) acc = __builtin_fmaf(w[k], a[k], acc);
+        } else {
+            float x, y, z;
+            if constexpr (SRC == 1) {
+                const float4 sp = D.pts[D.chunk0 + p];
+                x = sp.x; y = sp.y; z = sp.z;
+            } else {
+                const long i = D.chunk0 + p;
+                const float4 sp = D.pts[i >> 2];
+                const int q = (int)(i & 3);
+                const F3 pq = add3(mk3(sp.x, sp.y, sp.z),
+                                   mul3s(mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]), NORMAL_EPSILON));
+                x = pq.x; y = pq.y; z = pq.z;
+            }
+            const float a4[4] = {x, y, z, fr};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (k < in) acc = __builtin_fmaf(w[k], a4[k], acc);
+        }
+        float v = acc + D.b[o];
+        if (D.relu) v = fmaxf(v, 0.0f);
+        D.Z[t] = v;
+    }
+}
+
+// The first layer (in <= 4) on the matrix cores, for out >= 16.  v_mfma_f32_16x16x4_f32 is an
+// ascending-k fmaf chain over its four k (lane group g feeds k0 + g) accumulated onto C,
+// so one instruction per 4-k step, k0 = 0, 4, ..., gives every output exactly k_dense's
+// chain; k >= in is padded with zero weights AND zero activations (the fma then adds
+// +0 to a chain that is never -0).  A wave computes 32 outputs x 64 points (2 x 4
+// tiles) from the ray queues' positions (SRC 1 / 2, see k_dense).
+typedef float dense_f32x4 __attribute__((ext_vector_type(4)));
+template <int SRC>
+__global__ __launch_bounds__(256) void k_dense_mfma(DenseArgs D) {
+    const long n = D.count ? (long)(*D.count) * D.count_mul : D.n;
+    const long nc = min(n - D.chunk0, D.chunk_n);
+    if (nc <= 0) return;
+    const int in = D.in, out = D.out;
+    const int lane = lane_id(), j = lane & 15, g = lane >> 4;
+    const int oblocks = (out + 31) >> 5;
+    const long units = ((nc + 63) >> 6) * oblocks;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    float fr = 0.0f;
+    if constexpr (SRC != 0) fr = (float)D.args->frame;
+    for (long u = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; u < units; u += nwaves) {
+        const long pb = u / oblocks;
+        const int o0 = (int)(u - pb * oblocks) * 32;
+        const long p0 = pb * 64;
+        dense_f32x4 c[2][4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) c[mt][t] = dense_f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const float *wrow[2];
+        bool wok[2], pok[4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            wok[mt] = o0 + 16 * mt + j < out;
+            wrow[mt] = D.W + (long)(wok[mt] ? o0 + 16 * mt + j : 0) * in;
+        }
+        {
+            // layer 0: in <= 4, one k-step; lane (j, g) feeds input g of point j
+            float w[2], a[4];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) w[mt] = (g < in && wok[mt]) ? wrow[mt][g] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const long p = p0 + 16 * t + j;
+                pok[t] = p < nc;
+                float x = 0.0f, y = 0.0f, z = 0.0f;
+                if (pok[t]) {
+                    if constexpr (SRC == 1) {
+                        const float4 sp = D.pts[D.chunk0 + p];
+                        x = sp.x; y = sp.y; z = sp.z;
+                    } else {
+                        const long i = D.chunk0 + p;
+                        const float4 sp = D.pts[i >> 2];
+                        const int q = (int)(i & 3);
+                        const F3 pq = add3(mk3(sp.x, sp.y, sp.z),
+                                           mul3s(mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]), NORMAL_EPSILON));
+                        x = pq.x; y = pq.y; z = pq.z;
+                    }
+                }
+                const float v = g == 0 ? x : (g == 1 ? y : (g == 2 ? z : fr));
+                a[t] = (g < in && pok[t]) ? v : 0.0f;
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    c[mt][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt], a[t], c[mt][t], 0, 0, 0);
+        }
+        // lane (j, g), register r: output o0 + 16 mt + 4 g + r of point p0 + 16 t + j
+        const bool zvec = (out & 3) == 0 && ((uintptr_t)D.Z & 15) == 0;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const int o = o0 + 16 * mt + 4 * g;
+            float bias[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[r] = o + r < out ? D.b[o + r] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (!pok[t]) continue;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = c[mt][t][r] + bias[r];
+                    if (D.relu) v[r] = fmaxf(v[r], 0.0f);
+                }
+                float *zp = D.Z + (p0 + 16 * t + j) * (long)out + o;
+                if (zvec && o + 3 < out) {
+                    *reinterpret_cast<float4 *>(zp) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (o + r < out) zp[r] = v[r];
+                }
+            }
+        }
+    }
+}
+
+// Hidden layers (rows of D.A, out >= 16) on the matrix cores, LDS-tiled: a block
+// computes 64 outputs x 128 points; per 32-k chunk it stages the activation tile
+// [128][32] and the weight tile [64][32] (rows padded to 36 floats: the fragment reads
+// of 16 rows x 4 consecutive k hit 64 distinct banks) with coalesced float4 loads, then
+// each wave (32 outputs x 64 points) runs 8 k-steps of 2 x 4 v_mfma_f32_16x16x4_f32 in
+// ascending k.  Zero padding past `in` / `out` / the chunk end as in k_dense_mfma.
+constexpr int DT_P = 128, DT_O = 64, DT_K = 32, DT_S = 36;
+__device__ __forceinline__ void dense_stage(float *__restrict__ dst, const float *__restrict__ src, long rows_ok,
+                                            long row0, int ld, int kc, int nrows) {
+    // nrows x DT_K floats from src[(row0 + r) * ld + kc + c] into dst[r * DT_S + c]
+    const bool vec = (ld & 3) == 0 && ((uintptr_t)src & 15) == 0;
+    for (int i = threadIdx.x; i < nrows * (DT_K / 4); i += blockDim.x) {
+        const int r = i >> 3, c = (i & 7) * 4;
+        const long row = row0 + r;
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (row < rows_ok) {
+            const float *q = src + row * (long)ld + kc + c;
+            if (vec && kc + c + 3 < ld) {
+                v = *reinterpret_cast<const float4 *>(q);
+            } else {
+                v.x = kc + c < ld ? q[0] : 0.0f;
+                v.y = kc + c + 1 < ld ? q[1] : 0.0f;
+                v.z = kc + c + 2 < ld ? q[2] : 0.0f;
+                v.w = kc + c + 3 < ld ? q[3] : 0.0f;
+            }
+        }
+        *reinterpret_cast<float4 *>(dst + r * DT_S + c) = v;
+    }
+}
+__global__ __launch_bounds__(256) void k_dense_tiled(DenseArgs D) {
+    __shared__ __attribute__((aligned(16))) float sA[DT_P * DT_S];
+    __shared__ __attribute__((aligned(16))) float sW[DT_O * DT_S];
+    const long n = D.count ? (long)(*D.count) * D.count_mul : D.n;
+    const long nc = min(n - D.chunk0, D.chunk_n);
+    if (nc <= 0) return;
+    const int in = D.in, out = D.out;
+    const int lane = lane_id(), j = lane & 15, g = lane >> 4;
+    const int wv = threadIdx.x >> 6, wo = (wv & 1) * 32, wp = (wv >> 1) * 64;
+    const int oblocks = (out + DT_O - 1) / DT_O;
+    const long tiles = ((nc + DT_P - 1) / DT_P) * oblocks;
+    for (long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        const long pb = tile / oblocks;
+        const int o0 = (int)(tile - pb * oblocks) * DT_O;
+        const long p0 = pb * DT_P;
+        dense_f32x4 c[2][4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) c[mt][t] = dense_f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int kc = 0; kc < in; kc += DT_K) {
+            __syncthreads();  // previous chunk's fragment reads are done
+            dense_stage(sA, D.A + p0 * (long)in, nc - p0, 0, in, kc, DT_P);
+            dense_stage(sW, D.W + (long)o0 * in, out - o0, 0, in, kc, DT_O);
+            __syncthreads();
+#pragma unroll
+            for (int ks = 0; ks < DT_K / 4; ++ks) {
+                float w[2], a[4];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) w[mt] = sW[(wo + 16 * mt + j) * DT_S + 4 * ks + g];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) a[t] = sA[(wp + 16 * t + j) * DT_S + 4 * ks + g];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        c[mt][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[mt], a[t], c[mt][t], 0, 0, 0);
+            }
+        }
+        const bool zvec = (out & 3) == 0 && ((uintptr_t)D.Z & 15) == 0;
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            const int o = o0 + wo + 16 * mt + 4 * g;
+            float bias[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[r] = o + r < out ? D.b[o + r] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const long p = p0 + wp + 16 * t + j;
+                if (p >= nc) continue;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = c[mt][t][r] + bias[r];
+                    if (D.relu) v[r] = fmaxf(v[r], 0.0f);
+                }
+                float *zp = D.Z + p * (long)out + o;
+                if (zvec && o + 3 < out) {
+                    *reinterpret_cast<float4 *>(zp) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (o + r < out) zp[r] = v[r];
+                }
+            }
+        }
+    }
+}
+
+// The one-output layer (the SDF) over rows of D.A: one lane per point runs the whole
+// ascending-k fmaf chain, reading its row from an LDS tile [256][32] (row stride 33:
+// the 64 lanes' scalar reads hit distinct banks) staged with coalesced loads.
+__global__ __launch_bounds__(256) void k_dense_col(DenseArgs D) {
+    __shared__ float sA[256 * 33];
+    const long n = D.count ? (long)(*D.count) * D.count_mul : D.n;
+    const long nc = min(n - D.chunk0, D.chunk_n);
+    if (nc <= 0) return;
+    const int in = D.in;
+    const float b = D.b[0];
+    for (long p0 = (long)blockIdx.x * 256; p0 < nc; p0 += (long)gridDim.x * 256) {
+        const long p = p0 + threadIdx.x;
+        float acc = 0.0f;
+        for (int kc = 0; kc < in; kc += 32) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < 256 * 32; i += 256) {
+                const int r = i >> 5, k = i & 31;
+                const long row = p0 + r;
+                sA[r * 33 + k] = (row < nc && kc + k < in) ? D.A[row * (long)in + kc + k] : 0.0f;
+            }
+            __syncthreads();
+            const int kn = min(32, in - kc);
+            for (int k = 0; k < kn; ++k) acc = __builtin_fmaf(D.W[kc + k], sA[threadIdx.x * 33 + k], acc);
+        }
+        float v = acc + b;
+        if (D.relu) v = fmaxf(v, 0.0f);
+        if (p < nc) D.Z[p] = v;
+    }
 }
 
 // initMarcher (:293-358) for the rows of one shard + compaction of hits.
-__global__ __launch_bounds__(256) void k_init(RenderArgs A, QueueArgs Q) {
+__device__ __forceinline__ void init_rays(const RenderArgs &A, const QueueArgs &Q) {
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long npix = (long)A.W * A.rows;
     bool hit = false;
@@ -278,45 +545,81 @@ __global__ __launch_bounds__(256) void k_init(RenderArgs A, QueueArgs Q) {
             hit = true;
         }
     }
-    uint32_t slot = wave_append(hit, Q.cnt_out);
-    if (hit) { Q.p_out[slot] = st_p; Q.d_out[slot] = st_d; }
+    const Slots sl = block_append2(hit, Q.cnt_out, false, nullptr);
+    if (hit) { Q.p_out[sl.a] = st_p; Q.d_out[sl.a] = st_d; }
+}
+__global__ __launch_bounds__(256) void k_init(RenderArgs A, QueueArgs Q) { init_rays(A, Q); }
+__global__ __launch_bounds__(256) void k_init_l(const RenderArgs *__restrict__ Ad, QueueArgs Q) { init_rays(*Ad, Q); }
+
+// singleMarch (:416-477) for one block of queue entries given their SDFs, + compaction
+// (block-uniform: every thread of the block calls it).
+__device__ __forceinline__ void march_rays(const RenderArgs &A, const QueueArgs &Q, int it, bool live, float4 sp,
+                                           float4 sd, float sdf) {
+    const bool can_shade = (it + 1) < A.max_steps;
+    bool alive = false, conv = false;
+    F3 p = mk3(sp.x, sp.y, sp.z);
+    float tfar = sp.w;
+    if (live) {
+        float tstep = scene_sdf(p, sdf, A.scene, sphere_zoff(A.frame));
+        tfar -= tstep;
+        if (tfar <= 0) {
+            // background: output already 0
+        } else {
+            p = add3(p, mul3s(mk3(sd.x, sd.y, sd.z), tstep));
+            if (tstep < MARCHING_EPSILON) conv = can_shade;  // mask = COLOR_MASK_VAL
+            else alive = true;
+        }
+    }
+    const Slots sl = block_append2(alive, Q.cnt_out, conv, Q.shade_cnt);
+    if (alive) { Q.p_out[sl.a] = make_float4(p.x, p.y, p.z, tfar); Q.d_out[sl.a] = sd; }
+    if (conv) { Q.shade_p[sl.b] = make_float4(p.x, p.y, p.z, 0.0f); Q.shade_d[sl.b] = sd; }
+    if (threadIdx.x == 0 && sl.nb != 0) atomicAdd(Q.shade_it + it, 1u);
+}
+
+// surfaceNormal (:361-377) + colour: lane (ray, q) holds tetrahedron point q's SDF.
+__device__ __forceinline__ void shade_rays(const RenderArgs &A, bool live, float4 sp, float4 sd, float sdf) {
+    const int lane = lane_id(), q = lane & 3;
+    F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
+    F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
+    F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sphere_zoff(A.frame)));
+    const int l0 = lane & ~3;
+    float c1x = __shfl(cq.x, l0 + 1), c1y = __shfl(cq.y, l0 + 1), c1z = __shfl(cq.z, l0 + 1);
+    float c2x = __shfl(cq.x, l0 + 2), c2y = __shfl(cq.y, l0 + 2), c2z = __shfl(cq.z, l0 + 2);
+    float c3x = __shfl(cq.x, l0 + 3), c3y = __shfl(cq.y, l0 + 3), c3z = __shfl(cq.z, l0 + 3);
+    if (live && q == 0) {
+        F3 acc = add3(add3(add3(cq, mk3(c1x, c1y, c1z)), mk3(c2x, c2y, c2z)), mk3(c3x, c3y, c3z));
+        F3 nrm = normalize3(acc);
+        uint32_t pix = __float_as_uint(sd.w);
+        A.out[pix] = shade_color(A, A.normal, nrm, mk3(sd.x, sd.y, sd.z));
+    }
 }
 
 // One march iteration over the live queue: MLP + singleMarch (:416-477) + compaction.
 __global__ __launch_bounds__(256) void k_march(RenderArgs A, MlpArgs M, QueueArgs Q, int prec, int it) {
     Smem S = stage_mlp(M, prec);
     const uint32_t n = *Q.cnt_in;
-    const int lane = lane_id();
-    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-    const bool can_shade = (it + 1) < A.max_steps;
     const float fr = (float)A.frame;
-    for (long base = wave * 64; base < (long)n; base += nwaves * 64) {
-        long i = base + lane;
+    for (long base = (long)blockIdx.x * blockDim.x; base < (long)n; base += (long)gridDim.x * blockDim.x) {
+        long i = base + threadIdx.x;
         bool live = i < (long)n;
         float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
         if (live) { sp = Q.p_in[i]; sd = Q.d_in[i]; }
         float sdf = mlp_wave(M, S.s32, S.slp, S.sfl, prec, sp.x, sp.y, sp.z, fr);
-        bool alive = false, conv = false;
-        F3 p = mk3(sp.x, sp.y, sp.z);
-        float tfar = sp.w;
-        if (live) {
-            float tstep = scene_sdf(p, sdf, A.scene, sphere_zoff(A.frame));
-            tfar -= tstep;
-            if (tfar <= 0) {
-                // background: output already 0
-            } else {
-                p = add3(p, mul3s(mk3(sd.x, sd.y, sd.z), tstep));
-                if (tstep < MARCHING_EPSILON) conv = can_shade;  // mask = COLOR_MASK_VAL
-                else alive = true;
-            }
-        }
-        uint32_t so = wave_append(alive, Q.cnt_out);
-        if (alive) { Q.p_out[so] = make_float4(p.x, p.y, p.z, tfar); Q.d_out[so] = sd; }
-        uint32_t ss = wave_append(conv, Q.shade_cnt);
-        if (conv) { Q.shade_p[ss] = make_float4(p.x, p.y, p.z, 0.0f); Q.shade_d[ss] = sd; }
-        const uint64_t cm = __ballot(conv);
-        if (cm != 0ull && lane == __ffsll((unsigned long long)cm) - 1) atomicAdd(Q.shade_it + it, 1u);
+        march_rays(A, Q, it, live, sp, sd, sdf);
+    }
+}
+
+// Layered schedule: the same step with the SDFs the dense-layer chain left in sdf[].
+__global__ __launch_bounds__(256) void k_march_l(const RenderArgs *__restrict__ Ad, QueueArgs Q,
+                                                 const float *__restrict__ sdf, int it) {
+    const uint32_t n = *Q.cnt_in;
+    for (long base = (long)blockIdx.x * blockDim.x; base < (long)n; base += (long)gridDim.x * blockDim.x) {
+        long i = base + threadIdx.x;
+        bool live = i < (long)n;
+        float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
+        float v = 0.0f;
+        if (live) { sp = Q.p_in[i]; sd = Q.d_in[i]; v = sdf[i]; }
+        march_rays(*Ad, Q, it, live, sp, sd, v);
     }
 }
 
@@ -337,17 +640,24 @@ __global__ __launch_bounds__(256) void k_shade(RenderArgs A, MlpArgs M, QueueArg
         F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
         F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
         float sdf = mlp_fp32_wave(S.s32, M.in0, M.nh, pq.x, pq.y, pq.z, fr);
-        F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sphere_zoff(A.frame)));
-        const int l0 = lane & ~3;
-        float c1x = __shfl(cq.x, l0 + 1), c1y = __shfl(cq.y, l0 + 1), c1z = __shfl(cq.z, l0 + 1);
-        float c2x = __shfl(cq.x, l0 + 2), c2y = __shfl(cq.y, l0 + 2), c2z = __shfl(cq.z, l0 + 2);
-        float c3x = __shfl(cq.x, l0 + 3), c3y = __shfl(cq.y, l0 + 3), c3z = __shfl(cq.z, l0 + 3);
-        if (live && q == 0) {
-            F3 acc = add3(add3(add3(cq, mk3(c1x, c1y, c1z)), mk3(c2x, c2y, c2z)), mk3(c3x, c3y, c3z));
-            F3 nrm = normalize3(acc);
-            uint32_t pix = __float_as_uint(sd.w);
-            A.out[pix] = shade_color(A, A.normal, nrm, mk3(sd.x, sd.y, sd.z));
-        }
+        shade_rays(A, live, sp, sd, sdf);
+    }
+}
+
+// Layered schedule: colour the converged rays from the tetrahedron SDFs in sdf4[4 r + q].
+__global__ __launch_bounds__(256) void k_shade_l(const RenderArgs *__restrict__ Ad, QueueArgs Q,
+                                                 const float *__restrict__ sdf4) {
+    const uint32_t n = *Q.shade_cnt;
+    const int lane = lane_id();
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    for (long base = wave * 16; base < (long)n; base += nwaves * 16) {
+        long r = base + (lane >> 2);
+        bool live = r < (long)n;
+        float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
+        float v = 0.0f;
+        if (live) { sp = Q.shade_p[r]; sd = Q.shade_d[r]; v = sdf4[4 * r + (lane & 3)]; }
+        shade_rays(*Ad, live, sp, sd, v);
     }
 }
 
@@ -371,11 +681,30 @@ hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long
     hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(256), smem_bytes(M, prec), st, M, prec, X, Y, n);
     return hipGetLastError();
 }
-hipError_t launch_dense(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
-                        hipStream_t st) {
-    long tot = n * out;
-    if (tot <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dense, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, W, b, A, Z, n, in, out, relu);
+int dense_lds_bytes(int in, int out) {
+    const long b = (long)out * (in + 1) * 4;
+    return b <= 64 * 1024 ? (int)b : 0;
+}
+hipError_t launch_dense(const DenseArgs &D0, int src, int grid, hipStream_t st) {
+    DenseArgs D = D0;
+    if (src == 0 && D.out >= 16) {  // LDS-tiled matrix-core layer, grid-stride over 64 x 128 tiles
+        hipLaunchKernelGGL(k_dense_tiled, dim3(grid), dim3(256), 0, st, D);
+        return hipGetLastError();
+    }
+    if (src == 0 && D.out == 1) {
+        hipLaunchKernelGGL(k_dense_col, dim3(grid), dim3(256), 0, st, D);
+        return hipGetLastError();
+    }
+    if (D.out >= 16) {  // first layer on the matrix cores: 32-output x 64-point wave units
+        if (src == 1) hipLaunchKernelGGL(k_dense_mfma<1>, dim3(grid), dim3(256), 0, st, D);
+        else hipLaunchKernelGGL(k_dense_mfma<2>, dim3(grid), dim3(256), 0, st, D);
+        return hipGetLastError();
+    }
+    const int lds = dense_lds_bytes(D.in, D.out);
+    D.lds = lds > 0;
+    if (src == 0) hipLaunchKernelGGL(k_dense<0>, dim3(grid), dim3(256), lds, st, D);
+    else if (src == 1) hipLaunchKernelGGL(k_dense<1>, dim3(grid), dim3(256), lds, st, D);
+    else hipLaunchKernelGGL(k_dense<2>, dim3(grid), dim3(256), lds, st, D);
     return hipGetLastError();
 }
 hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st) {
@@ -387,6 +716,27 @@ hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st) 
 hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int prec, int it, int grid,
                         hipStream_t st) {
     hipLaunchKernelGGL(k_march, dim3(grid), dim3(256), smem_bytes(M, prec), st, A, M, Q, prec, it);
+    return hipGetLastError();
+}
+__global__ void k_set_args(RenderArgs A, RenderArgs *d) {
+    if (threadIdx.x == 0) *d = A;
+}
+hipError_t launch_set_args(const RenderArgs &A, RenderArgs *d, hipStream_t st) {
+    hipLaunchKernelGGL(k_set_args, dim3(1), dim3(64), 0, st, A, d);
+    return hipGetLastError();
+}
+hipError_t launch_init_l(const RenderArgs *Ad, const QueueArgs &Q, long npix, hipStream_t st) {
+    if (npix <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_init_l, dim3((unsigned)((npix + 255) / 256)), dim3(256), 0, st, Ad, Q);
+    return hipGetLastError();
+}
+hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf, int it, int grid,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_march_l, dim3(grid), dim3(256), 0, st, Ad, Q, sdf, it);
+    return hipGetLastError();
+}
+hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(k_shade_l, dim3(grid), dim3(256), 0, st, Ad, Q, sdf4);
     return hipGetLastError();
 }
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st) {

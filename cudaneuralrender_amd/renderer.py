@@ -187,8 +187,9 @@ class Renderer:
         return p.as_dict()
 
     def set_schedule(self, schedule):
-        """"persistent" (one k_trace launch per frame, default) or "wavefront" (one
-        k_march launch per iteration)."""
+        """"persistent" (one k_trace launch per frame, default), "wavefront" (one
+        k_march launch per iteration) or "layered" (one dense-layer launch per layer per
+        iteration, replayed as a hipGraph; networks of other shapes always use it)."""
         self._chk(self._L.nr_set_schedule(self._ctx, NR_SCHEDULE[schedule] if isinstance(schedule, str) else schedule))
         return self
 
@@ -222,6 +223,11 @@ class Renderer:
     def set_queue_shards(self, n):
         """Persistent schedule: number of pixel-queue counters (power of two <= 64)."""
         self._chk(self._L.nr_set_queue_shards(self._ctx, int(n)))
+        return self
+
+    def set_layer_chunk(self, points=0):
+        """Layered schedule: points per dense-layer launch (0 = auto)."""
+        self._chk(self._L.nr_set_layer_chunk(self._ctx, int(points)))
         return self
 
     def set_temporal_order(self, on=True):

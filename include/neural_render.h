@@ -50,6 +50,10 @@ extern "C" {
 /* march schedule (nr_set_schedule) */
 #define NR_SCHED_PERSISTENT 0 /* one persistent k_trace launch per frame (default) */
 #define NR_SCHED_WAVEFRONT 1  /* one k_march launch per iteration over a compacted ray queue */
+#define NR_SCHED_LAYERED 2    /* the reference's structure: per iteration one dense-layer launch per
+                                 layer over the live-ray queue, then the step; replayed as a hipGraph.
+                                 Any dense [3|4, ..., 1] network, fp32.  Networks the fused kernels
+                                 do not take ([3|4, 32, ..., 32, 1]) always render this way. */
 
 /* buffer location flags */
 #define NR_HOST 0
@@ -109,7 +113,10 @@ int nr_set_matcap(nr_ctx *ctx, const uint32_t *rgba, int w, int h);
 /* Replaces render_kernel (volumeRender_kernel.cu:608-692): renders a W x H frame,
  * at most max_steps march iterations (reference MAX_STEPS = 6000), into out
  * (W*H packed RGBA, row y*W + x, unconverged / missed pixels 0).  out_loc is
- * NR_HOST or NR_DEVICE.  stats may be NULL. */
+ * NR_HOST or NR_DEVICE.  stats may be NULL.  Any dense network with 3 or 4 inputs and
+ * one output renders (NeuralNetwork takes any layer list, neuralNetwork.cpp:85-151):
+ * [3|4, 32, ..., 32, 1] on the fused kernels of the selected schedule, every other
+ * shape on NR_SCHED_LAYERED. */
 int nr_render(nr_ctx *ctx, uint32_t *out, int W, int H, int max_steps, int out_loc,
               nr_stats *stats);
 /* Multi-GPU shard of a frame: rows are dealt in bands of band_rows, band b goes to
@@ -179,7 +186,8 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * MLP latency probe: nr_mlp_forward(X >= 64 points, Y >= 65 floats, n = repetitions, on
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
  * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
- * layer. */
+ * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
+ * the captured hipGraph (for profilers that do not follow graph launches). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are
@@ -195,6 +203,10 @@ int nr_set_wave_rays(nr_ctx *ctx, int rays);
 /* Pixel-queue shards (persistent schedule; power of two <= 64, default 8): the queue's
  * atomic counters, each on its own 128-byte line, that the waves take pixels from. */
 int nr_set_queue_shards(nr_ctx *ctx, int n);
+/* NR_SCHED_LAYERED: points per dense-layer launch (the activations of one chunk are the
+ * layer scratch: 2 x points x widest hidden layer x 4 B).  0 = auto (128 MiB per buffer).
+ * The reference sizes Z for the whole batch, W*H*4 points (volumeRender_kernel.cu:659-661). */
+int nr_set_layer_chunk(nr_ctx *ctx, long points);
 /* Age hold (persistent schedule): a wave holding a ray that has marched `age` or more
  * iterations stops taking new pixels, packs its live rays into the fewest 16-ray tiles
  * and raises its issue priority to `prio` (0-3) until they finish, so long rays march

@@ -80,7 +80,7 @@ RENDER_CASES = [
 ]
 
 
-@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront", "layered"])
 @pytest.mark.parametrize("W,H,scene,color,rx,ry,zoom,steps", RENDER_CASES)
 def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, steps, schedule):
     dims, K, B = nets["plane_1"]
@@ -178,17 +178,19 @@ def test_render_lowp_close(rend, nets, chrome, prec, schedule):
 
 
 def test_schedules_agree_1024(rend, nets, chrome):
-    # full benchmark frame: persistent and wavefront schedules give identical pixels/stats
+    # full benchmark frame: persistent, wavefront and layered schedules give identical
+    # pixels/stats
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision("fp32")
     iv, nm = nr.camera(0, 0, 2)
     rend.set_view(iv, nm).set_static(1, 3).set_scene("v1").set_matcap(chrome)
     a, sa = rend.set_schedule("persistent").render(1024, 1024, 128)
     b, sb = rend.set_schedule("wavefront").render(1024, 1024, 128)
+    c, sc = rend.set_schedule("layered").render(1024, 1024, 128)
     rend.set_schedule("persistent")
-    assert np.array_equal(a, b)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
     for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
-        assert sa[k] == sb[k], (k, sa, sb)
+        assert sa[k] == sb[k] == sc[k], (k, sa, sb, sc)
 
 
 @pytest.mark.parametrize("W,H", [(200, 131), (1024, 1024)])
