@@ -28,7 +28,7 @@ __device__ __forceinline__ float tile_outputs(const float zt[4]) {
 
 // FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
 // PART != 0 only in the latency diagnostic (nr_diag.hip): stop after the hidden layers.
-template <int NT, int PART = 0, int NH = 0>
+template <int NT, int PART = 0>
 __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
                                                float y, float z) {
     // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
@@ -59,7 +59,7 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
     }
     // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
-    auto hidden = [&](int jl) {
+    for (int jl = 0; jl < nh; ++jl) {
         const float *L = s + PK_HID + jl * PK_HID_STRIDE;
         float4 wq[4];
 #pragma unroll
@@ -86,14 +86,6 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
-    };
-    if constexpr (NH > 0) {
-        // fully unrolled: the next layer's weight loads and first k-steps can be
-        // scheduled into the previous layer's epilogue
-#pragma unroll
-        for (int jl = 0; jl < NH; ++jl) hidden(jl);
-    } else {
-        for (int jl = 0; jl < nh; ++jl) hidden(jl);
     }
     if constexpr (PART != 0) return a[0][0] + a[NT - 1][7];
     // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
@@ -124,7 +116,7 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
 __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
                                             float z, uint32_t tmask) {
     const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
-    if (nt >= 4) return nh == 7 ? mlp16_fp32_nt<4, 0, 7>(s, in0, nh, fr, x, y, z) : mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
+    if (nt >= 4) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
     if (nt == 3) return mlp16_fp32_nt<3>(s, in0, nh, fr, x, y, z);
     if (nt == 2) return mlp16_fp32_nt<2>(s, in0, nh, fr, x, y, z);
     return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
