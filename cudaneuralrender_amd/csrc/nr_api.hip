@@ -218,9 +218,6 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
 int ensure_rays(nr_ctx *c, size_t n) {
     if (n <= c->cap_rays) return NR_OK;
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    if (c->h_frames) (void)hipHostFree(c->h_frames);
-    if (c->ev_frames) (void)hipEventDestroy(c->ev_frames);
-    dfree(c->d_frames); dfree(c->d_bout);
     dfree(c->d_SP); dfree(c->d_SD);
     c->cap_rays = 0;
     size_t b = std::max<size_t>(n, 64) * sizeof(float4);
@@ -282,6 +279,143 @@ int num_cus(int dev) {
 }
 
 
+int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
+
+// Per-frame arguments of a batch: pinned staging (reused only once the previous upload
+// has been consumed) + device copy.  With host outputs the frames of one launch go
+// through d_bout (`chunk` frames).
+int upload_frames(nr_ctx *c, const nr_frame *frames, int nframes, size_t npix, int loc, int chunk, hipStream_t s) {
+    if (!c->ev_frames) HIPCHK(c, hipEventCreateWithFlags(&c->ev_frames, hipEventDisableTiming));
+    HIPCHK(c, hipEventSynchronize(c->ev_frames));
+    if ((size_t)nframes > c->cap_frames) {
+        if (c->h_frames) HIPCHK(c, hipHostFree(c->h_frames));
+        dfree(c->d_frames);
+        c->h_frames = nullptr;
+        c->cap_frames = 0;
+        HIPCHK(c, hipHostMalloc(&c->h_frames, (size_t)nframes * sizeof(FrameArgs)));
+        HIPCHK(c, hipMalloc(&c->d_frames, (size_t)nframes * sizeof(FrameArgs)));
+        c->cap_frames = nframes;
+    }
+    int rc;
+    if (loc != NR_DEVICE && (rc = ensure_buf(c, c->d_bout, c->cap_bout, npix * chunk)) != NR_OK) return rc;
+    for (int i = 0; i < nframes; ++i) {
+        FrameArgs &f = c->h_frames[i];
+        memcpy(f.inv_view, frames[i].inv_view, sizeof f.inv_view);
+        memcpy(f.normal, frames[i].normal, sizeof f.normal);
+        f.zoff = -0.7 + ((double)(frames[i].frame * 2) * 0.7 / 360.0);  // sphere_zoff, same f64 ops
+        f.frame = frames[i].frame;
+        f.frame_f = (float)frames[i].frame;
+        f.out = loc == NR_DEVICE ? frames[i].out : c->d_bout + (size_t)(i % chunk) * npix;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_frames, c->h_frames, (size_t)nframes * sizeof(FrameArgs), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipEventRecord(c->ev_frames, s));
+    return NR_OK;
+}
+
+// Wavefront schedule over the frames of a batch (one frame for nr_render_shard): the
+// rays of up to 32 frames share one queue; per iteration ONE k_march16 launch (mlp16 +
+// step + compaction) over it, at the end k_shade16.  The host polls the live count every
+// check_every iterations and stops early once it is 0.
+int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H, int band, int nshards, int shard,
+                     int max_steps, int loc, nr_stats *stats, hipStream_t s) {
+    const int rows = nr_shard_rows(H, band, nshards, shard);
+    const size_t npix = (size_t)W * rows;
+    nr_stats tot{};
+    if (npix == 0) { if (stats) *stats = tot; return NR_OK; }
+    if (npix > (1u << 27))
+        return set_err(c, NR_E_INVALID, "nr_render: the wavefront schedule takes at most 2^27 pixels per shard");
+    const int chunk = std::min(nframes, NR_MAX_BATCH);
+    // WF_SEGS queue segments of seg_cap entries (a multiple of the 256-thread block)
+    const size_t seg_cap = ((npix * chunk + WF_SEGS - 1) / WF_SEGS + 255) / 256 * 256;
+    // counters: (max_steps + 1) x [WF_SEGS live counts], [WF_SEGS shade counts], then
+    // max_steps shade flags; each count on its own 128-byte line
+    const size_t line = (size_t)WF_SEGS * 32;
+    const size_t nctr = (size_t)(max_steps + 2) * line + max_steps;
+    int rc;
+    if ((rc = ensure_rays(c, seg_cap * WF_SEGS)) != NR_OK) return rc;
+    if ((rc = ensure_ctr(c, nctr + 8)) != NR_OK) return rc;
+    if ((rc = upload_frames(c, frames, nframes, npix, loc, chunk, s)) != NR_OK) return rc;
+    RenderArgs A{};
+    A.out = nullptr; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
+    A.max_steps = max_steps; A.scene = c->scene; A.frame = 0; A.color_type = c->color_type;
+    A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    const int cus = num_cus(c->device);
+    const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 16;  // measured: 4 -> 2.10, 8 -> 2.06, 16 -> 2.02 ms/frame (32-frame batch)
+    uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + (size_t)(max_steps + 1) * line,
+             *shade_it = c->d_ctr + (size_t)(max_steps + 2) * line;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    for (int f0 = 0; f0 < nframes; f0 += chunk) {
+        const int n = std::min(chunk, nframes - f0);
+        const FrameArgs *F = c->d_frames + f0;
+        const size_t total = npix * n;
+        HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, nctr * 4, s));
+        QueueArgs Q{};
+        Q.seg_cap = (long)seg_cap;
+        Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
+        Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
+        if ((rc = prof_begin(c, 0, s)) != NR_OK) return rc;
+        HIPCHK(c, launch_init_f(A, F, Q, (long)npix, (long)total, s));
+        if ((rc = prof_end(c, s)) != NR_OK) return rc;
+        tot.launches += 2;
+        const int grid = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, (size_t)cus * bpc));
+        for (int it = 0; it < max_steps; ++it) {
+            Q.cnt_in = cnt + (size_t)it * line; Q.cnt_out = cnt + (size_t)(it + 1) * line;
+            Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
+            Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
+            if ((rc = prof_begin(c, 1, s)) != NR_OK) return rc;
+            HIPCHK(c, launch_march16(A, c->mlp16, Q, F, c->precision, it, grid, s));
+            if ((rc = prof_end(c, s)) != NR_OK) return rc;
+            ++tot.launches;
+            if (c->check_every > 0 && (it + 1) % c->check_every == 0 && it + 1 < max_steps) {
+                HIPCHK(c, hipMemcpyAsync(c->h_ctr, Q.cnt_out, line * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(c, hipStreamSynchronize(s));
+                uint64_t live = 0;
+                for (int q = 0; q < WF_SEGS; ++q) live += c->h_ctr[q * 32];
+                if (live == 0) break;
+            }
+        }
+        const int shade_grid = (int)std::max<size_t>(1, std::min<size_t>((total + 1023) / 1024, (size_t)cus * 4));
+        if ((rc = prof_begin(c, 2, s)) != NR_OK) return rc;
+        HIPCHK(c, launch_shade16(A, c->mlp16, Q, F, shade_grid, s));
+        if ((rc = prof_end(c, s)) != NR_OK) return rc;
+        if (loc != NR_DEVICE)
+            for (int i = f0; i < f0 + n; ++i)
+                HIPCHK(c, hipMemcpyAsync(frames[i].out, c->d_bout + (size_t)(i % chunk) * npix, npix * 4,
+                                         hipMemcpyDeviceToHost, s));
+        if (stats) {
+            HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_ctr, nctr * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const uint32_t *h = c->h_ctr;
+            int iters = 0;
+            for (int it = 0; it < max_steps; ++it) {
+                uint64_t live = 0;
+                for (int q = 0; q < WF_SEGS; ++q) live += h[(size_t)it * line + q * 32];
+                tot.ray_steps += live;
+                if (it == 0) tot.rays_hit += live;
+                if (live) iters = std::max(iters, it + 1);
+                if (h[(size_t)(max_steps + 2) * line + it]) iters = std::max(iters, std::min(it + 2, max_steps));
+            }
+            uint64_t shaded = 0;
+            for (int q = 0; q < WF_SEGS; ++q) shaded += h[(size_t)(max_steps + 1) * line + q * 32];
+            tot.rays_shaded += shaded;
+            tot.shade_evals += 4 * shaded;
+            tot.iterations = std::max(tot.iterations, iters);
+        }
+    }
+    if (c->profiling) c->prof_renders += nframes;
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    if (stats) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        tot.ms_total = ms;
+        *stats = tot;
+    } else if (loc != NR_DEVICE) {
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    return NR_OK;
+}
+
 // one dense layer over n rows (k_dense<0>)
 hipError_t dense_rows(const float *W, const float *b, const float *A, float *Z, long n, int in, int out, int relu,
                       int cus, hipStream_t s) {
@@ -293,13 +427,11 @@ hipError_t dense_rows(const float *W, const float *b, const float *A, float *Z, 
     return launch_dense(D, 0, grid, s);
 }
 
-// stats of the queue schedules (wavefront, layered) from their per-iteration counters
-int queue_stats(nr_ctx *c, int max_steps, int launches, nr_stats *stats, hipStream_t s) {
-    if (!stats) return NR_OK;
+// counts of the queue schedules (wavefront, layered) from their per-iteration counters
+int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s) {
     const size_t nctr = (size_t)2 * max_steps + 2;
     HIPCHK(c, hipMemcpyAsync(c->h_ctr, c->d_ctr, nctr * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    nr_stats st{};
     uint64_t steps = 0;
     int iters = 0;
     for (int it = 0; it < max_steps; ++it) {
@@ -312,6 +444,13 @@ int queue_stats(nr_ctx *c, int max_steps, int launches, nr_stats *stats, hipStre
     st.rays_shaded = c->h_ctr[max_steps + 1];
     st.shade_evals = 4ull * st.rays_shaded;
     st.iterations = iters;
+    return NR_OK;
+}
+int queue_stats(nr_ctx *c, int max_steps, int launches, nr_stats *stats, hipStream_t s) {
+    if (!stats) return NR_OK;
+    nr_stats st{};
+    int rc = read_queue_counters(c, max_steps, st, s);
+    if (rc != NR_OK) return rc;
     st.launches = launches;
     float ms = 0;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
@@ -486,6 +625,9 @@ int nr_destroy(nr_ctx *c) {
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
     dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
+    dfree(c->d_frames); dfree(c->d_bout);
+    if (c->h_frames) (void)hipHostFree(c->h_frames);
+    if (c->ev_frames) (void)hipEventDestroy(c->ev_frames);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -603,7 +745,15 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (W < 1 || H < 1 || (long)W * H > (1l << 31)) return set_err(c, NR_E_INVALID, "nr_render: bad size %dx%d", W, H);
     if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
     if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
-    if (c->schedule != NR_SCHED_PERSISTENT || !c->fused || (c->debug & (1 | 8))) {
+    if (c->schedule == NR_SCHED_WAVEFRONT && c->fused && !(c->debug & 2)) {
+        if (c->dims[0] != c->num_inputs)
+            return set_err(c, NR_E_STATE, "nr_render: network takes %d inputs but numInputs = %d", c->dims[0], c->num_inputs);
+        if (c->color_type == NR_COLOR_MATCAP && !c->d_matcap) return set_err(c, NR_E_STATE, "nr_render: matcap colouring without a matcap");
+        HIPCHK(c, hipSetDevice(c->device));
+        GET_STREAM(c, s);
+        return render_wavefront(c, frames, nframes, W, H, band, nshards, shard, max_steps, loc, stats, s);
+    }
+    if (c->schedule != NR_SCHED_PERSISTENT || !c->fused || (c->debug & (1 | 2 | 8))) {
         // frame by frame (the wavefront and layered schedules and the diagnostics are
         // single-frame)
         float iv[12], nm[16];
@@ -642,31 +792,8 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (npix == 0) { if (stats) *stats = st; return NR_OK; }
     GET_STREAM(c, s);
     int rc;
-    // per-frame arguments: pinned staging (reused only once the previous upload is done)
-    if (!c->ev_frames) HIPCHK(c, hipEventCreateWithFlags(&c->ev_frames, hipEventDisableTiming));
-    HIPCHK(c, hipEventSynchronize(c->ev_frames));
-    if ((size_t)nframes > c->cap_frames) {
-        if (c->h_frames) HIPCHK(c, hipHostFree(c->h_frames));
-        dfree(c->d_frames);
-        c->h_frames = nullptr;
-        c->cap_frames = 0;
-        HIPCHK(c, hipHostMalloc(&c->h_frames, (size_t)nframes * sizeof(FrameArgs)));
-        HIPCHK(c, hipMalloc(&c->d_frames, (size_t)nframes * sizeof(FrameArgs)));
-        c->cap_frames = nframes;
-    }
     const int chunk = std::min(nframes, NR_MAX_BATCH);
-    if (loc != NR_DEVICE && (rc = ensure_buf(c, c->d_bout, c->cap_bout, npix * chunk)) != NR_OK) return rc;
-    for (int i = 0; i < nframes; ++i) {
-        FrameArgs &f = c->h_frames[i];
-        memcpy(f.inv_view, frames[i].inv_view, sizeof f.inv_view);
-        memcpy(f.normal, frames[i].normal, sizeof f.normal);
-        f.zoff = -0.7 + ((double)(frames[i].frame * 2) * 0.7 / 360.0);  // sphere_zoff, same f64 ops
-        f.frame = frames[i].frame;
-        f.frame_f = (float)frames[i].frame;
-        f.out = loc == NR_DEVICE ? frames[i].out : c->d_bout + (size_t)(i % chunk) * npix;
-    }
-    HIPCHK(c, hipMemcpyAsync(c->d_frames, c->h_frames, (size_t)nframes * sizeof(FrameArgs), hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipEventRecord(c->ev_frames, s));
+    if ((rc = upload_frames(c, frames, nframes, npix, loc, chunk, s)) != NR_OK) return rc;
 
     RenderArgs A{};
     A.out = nullptr; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
@@ -884,7 +1011,22 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         }
         return NR_OK;
     }
-    // ---- wavefront schedule: one k_march launch per iteration
+    if (!(c->debug & 2)) {
+        // ---- wavefront schedule (16-point tiles, render_wavefront) on this one frame
+        nr_frame fr{};
+        memcpy(fr.inv_view, c->inv_view, sizeof fr.inv_view);
+        memcpy(fr.normal, c->normal, sizeof fr.normal);
+        fr.frame = c->frame;
+        fr.out = dout;
+        if ((rc2 = render_wavefront(c, &fr, 1, W, H, band, nshards, shard, max_steps, NR_DEVICE, stats, s)) != NR_OK)
+            return rc2;
+        if (loc != NR_DEVICE) {
+            HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+        }
+        return NR_OK;
+    }
+    // ---- debug bit 1: the 32-point-tile wavefront kernels (k_march / k_shade), kept for comparison
     // counters: [0, max_steps] live counts, [max_steps+1] shade count, [max_steps+2 ...] shade_it
     uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + max_steps + 1, *shade_it = c->d_ctr + max_steps + 2;
     size_t nctr = (size_t)2 * max_steps + 2;

@@ -35,7 +35,10 @@ struct QueueArgs {
     uint32_t *shade_cnt;
     float4 *shade_p, *shade_d;
     uint32_t *shade_it;     // per-iteration count of waves that enqueued converged rays
+    long seg_cap;           // segmented queues (wavefront schedule): WF_SEGS segments of
+                            // seg_cap entries, one counter each (cnt_*[s], shade_cnt[s])
 };
+constexpr int WF_SEGS = 8;
 
 // One dense layer over a chunk of points (k_dense; layered schedule and the generic
 // nr_mlp_forward).  Z is chunk-local [chunk][out].
@@ -93,6 +96,12 @@ int smem_bytes(const MlpArgs &M, int prec);
 hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
 int dense_lds_bytes(int in, int out);
 hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
+hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
+                         hipStream_t st);
+hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
+                          int it, int grid, hipStream_t st);
+hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int grid,
+                          hipStream_t st);
 hipError_t launch_set_args(const RenderArgs &A, RenderArgs *d, hipStream_t st);
 hipError_t launch_init_l(const RenderArgs *Ad, const QueueArgs &Q, long npix, hipStream_t st);
 hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf, int it, int grid, hipStream_t st);

@@ -26,7 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "nr_device.h"
+#include "nr_mlp16.h"
 
 namespace nr {
 
@@ -511,39 +511,44 @@ __global__ __launch_bounds__(256) void k_dense_col(DenseArgs D) {
     }
 }
 
-// initMarcher (:293-358) for the rows of one shard + compaction of hits.
+// initMarcher (:293-358) for pixel t of the shard, camera M (3x4): the ray's queue
+// entry {p, tfar}, {d, -} if it hits the bounding sphere.
+__device__ __forceinline__ bool gen_hit(const RenderArgs &A, const float *M, long t, float4 &st_p, float4 &st_d) {
+    int lr = (int)(t / A.W), x = (int)(t - (long)lr * A.W);
+    int y = ((lr / A.band) * A.nshards + A.shard) * A.band + (lr % A.band);
+    F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
+               dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
+    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
+    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
+    F3 d = normalize3(mk3(u, v, -2.0f));
+    d = mk3(dot3(d, mk3(M[0], M[1], M[2])), dot3(d, mk3(M[4], M[5], M[6])), dot3(d, mk3(M[8], M[9], M[10])));
+    // intersectSphere (:199-215), bounding sphere c = 0, r = 1.2
+    F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
+    float a = dot3(d, d);
+    float b = (float)(2.0 * (double)dot3(Qv, d));
+    float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
+    float disc = b * b - 4 * a * cc;
+    if (!(disc > 0)) return false;
+    float sq = sqrtf(disc);
+    float tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
+    float tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
+    if (tnear < 0.0f) tnear = 0.0f;
+    F3 p = add3(o, mul3s(d, tnear));
+    st_p = make_float4(p.x, p.y, p.z, tfar);
+    st_d = make_float4(d.x, d.y, d.z, 0.0f);
+    return true;
+}
+
+// one pixel per thread (block-uniform), hits appended to the queue tagged with the pixel
 __device__ __forceinline__ void init_rays(const RenderArgs &A, const QueueArgs &Q) {
     const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const long npix = (long)A.W * A.rows;
     bool hit = false;
     float4 st_p = make_float4(0, 0, 0, 0), st_d = make_float4(0, 0, 0, 0);
     if (t < npix) {
-        int lr = (int)(t / A.W), x = (int)(t - (long)lr * A.W);
-        int y = ((lr / A.band) * A.nshards + A.shard) * A.band + (lr % A.band);
         A.out[t] = 0u;  // caller's cudaMemset (main.cpp:408): misses and unconverged stay 0
-        const float *M = A.inv_view;
-        F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
-                   dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
-        float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
-        float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
-        F3 d = normalize3(mk3(u, v, -2.0f));
-        d = mk3(dot3(d, mk3(M[0], M[1], M[2])), dot3(d, mk3(M[4], M[5], M[6])), dot3(d, mk3(M[8], M[9], M[10])));
-        // intersectSphere (:199-215), bounding sphere c = 0, r = 1.2
-        F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
-        float a = dot3(d, d);
-        float b = (float)(2.0 * (double)dot3(Qv, d));
-        float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
-        float disc = b * b - 4 * a * cc;
-        if (disc > 0) {
-            float sq = sqrtf(disc);
-            float tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
-            float tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
-            if (tnear < 0.0f) tnear = 0.0f;
-            F3 p = add3(o, mul3s(d, tnear));
-            st_p = make_float4(p.x, p.y, p.z, tfar);
-            st_d = make_float4(d.x, d.y, d.z, __uint_as_float((uint32_t)t));
-            hit = true;
-        }
+        hit = gen_hit(A, A.inv_view, t, st_p, st_d);
+        st_d.w = __uint_as_float((uint32_t)t);
     }
     const Slots sl = block_append2(hit, Q.cnt_out, false, nullptr);
     if (hit) { Q.p_out[sl.a] = st_p; Q.d_out[sl.a] = st_d; }
@@ -554,13 +559,13 @@ __global__ __launch_bounds__(256) void k_init_l(const RenderArgs *__restrict__ A
 // singleMarch (:416-477) for one block of queue entries given their SDFs, + compaction
 // (block-uniform: every thread of the block calls it).
 __device__ __forceinline__ void march_rays(const RenderArgs &A, const QueueArgs &Q, int it, bool live, float4 sp,
-                                           float4 sd, float sdf) {
+                                           float4 sd, float sdf, double zoff) {
     const bool can_shade = (it + 1) < A.max_steps;
     bool alive = false, conv = false;
     F3 p = mk3(sp.x, sp.y, sp.z);
     float tfar = sp.w;
     if (live) {
-        float tstep = scene_sdf(p, sdf, A.scene, sphere_zoff(A.frame));
+        float tstep = scene_sdf(p, sdf, A.scene, zoff);
         tfar -= tstep;
         if (tfar <= 0) {
             // background: output already 0
@@ -573,15 +578,16 @@ __device__ __forceinline__ void march_rays(const RenderArgs &A, const QueueArgs 
     const Slots sl = block_append2(alive, Q.cnt_out, conv, Q.shade_cnt);
     if (alive) { Q.p_out[sl.a] = make_float4(p.x, p.y, p.z, tfar); Q.d_out[sl.a] = sd; }
     if (conv) { Q.shade_p[sl.b] = make_float4(p.x, p.y, p.z, 0.0f); Q.shade_d[sl.b] = sd; }
-    if (threadIdx.x == 0 && sl.nb != 0) atomicAdd(Q.shade_it + it, 1u);
+    if (threadIdx.x == 0 && sl.nb != 0) Q.shade_it[it] = 1u;  // a flag: plain stores, no atomic
 }
 
 // surfaceNormal (:361-377) + colour: lane (ray, q) holds tetrahedron point q's SDF.
-__device__ __forceinline__ void shade_rays(const RenderArgs &A, bool live, float4 sp, float4 sd, float sdf) {
+__device__ __forceinline__ void shade_rays(const RenderArgs &A, const float *nm, uint32_t *out, double zoff, bool live,
+                                           float4 sp, float4 sd, uint32_t pix, float sdf) {
     const int lane = lane_id(), q = lane & 3;
     F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
     F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
-    F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sphere_zoff(A.frame)));
+    F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff));
     const int l0 = lane & ~3;
     float c1x = __shfl(cq.x, l0 + 1), c1y = __shfl(cq.y, l0 + 1), c1z = __shfl(cq.z, l0 + 1);
     float c2x = __shfl(cq.x, l0 + 2), c2y = __shfl(cq.y, l0 + 2), c2z = __shfl(cq.z, l0 + 2);
@@ -589,8 +595,7 @@ __device__ __forceinline__ void shade_rays(const RenderArgs &A, bool live, float
     if (live && q == 0) {
         F3 acc = add3(add3(add3(cq, mk3(c1x, c1y, c1z)), mk3(c2x, c2y, c2z)), mk3(c3x, c3y, c3z));
         F3 nrm = normalize3(acc);
-        uint32_t pix = __float_as_uint(sd.w);
-        A.out[pix] = shade_color(A, A.normal, nrm, mk3(sd.x, sd.y, sd.z));
+        out[pix] = shade_color(A, nm, nrm, mk3(sd.x, sd.y, sd.z));
     }
 }
 
@@ -605,7 +610,7 @@ __global__ __launch_bounds__(256) void k_march(RenderArgs A, MlpArgs M, QueueArg
         float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
         if (live) { sp = Q.p_in[i]; sd = Q.d_in[i]; }
         float sdf = mlp_wave(M, S.s32, S.slp, S.sfl, prec, sp.x, sp.y, sp.z, fr);
-        march_rays(A, Q, it, live, sp, sd, sdf);
+        march_rays(A, Q, it, live, sp, sd, sdf, sphere_zoff(A.frame));
     }
 }
 
@@ -619,7 +624,7 @@ __global__ __launch_bounds__(256) void k_march_l(const RenderArgs *__restrict__ 
         float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
         float v = 0.0f;
         if (live) { sp = Q.p_in[i]; sd = Q.d_in[i]; v = sdf[i]; }
-        march_rays(*Ad, Q, it, live, sp, sd, v);
+        march_rays(*Ad, Q, it, live, sp, sd, v, sphere_zoff(Ad->frame));
     }
 }
 
@@ -640,7 +645,7 @@ __global__ __launch_bounds__(256) void k_shade(RenderArgs A, MlpArgs M, QueueArg
         F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
         F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
         float sdf = mlp_fp32_wave(S.s32, M.in0, M.nh, pq.x, pq.y, pq.z, fr);
-        shade_rays(A, live, sp, sd, sdf);
+        shade_rays(A, A.normal, A.out, sphere_zoff(A.frame), live, sp, sd, __float_as_uint(sd.w), sdf);
     }
 }
 
@@ -657,7 +662,119 @@ __global__ __launch_bounds__(256) void k_shade_l(const RenderArgs *__restrict__ 
         float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
         float v = 0.0f;
         if (live) { sp = Q.shade_p[r]; sd = Q.shade_d[r]; v = sdf4[4 * r + (lane & 3)]; }
-        shade_rays(*Ad, live, sp, sd, v);
+        shade_rays(*Ad, Ad->normal, Ad->out, sphere_zoff(Ad->frame), live, sp, sd, __float_as_uint(sd.w), v);
+    }
+}
+
+// ------------------------------------ wavefront schedule on the 16-point-tile MLP
+// One queue holds the rays of one frame or of up to 32 (nr_render_batch): entry
+// {x, y, z, tfar}, {dx, dy, dz, tag}, tag = pixel | frame << WF_FSHIFT; a ray's camera,
+// sphere offset, 4th network input and output image come from F[frame].  The queue is
+// split into WF_SEGS segments of seg_cap entries with a counter each: pixel t starts in
+// segment t / seg_cap and its ray stays there (survivors and converged rays of a
+// segment never outnumber its pixels), so the appends of a block go to one of 8
+// counters on their own cache lines instead of all to one (same-address atomics
+// serialise at ~10 ns; 32 frames = 131k appending blocks per iteration).
+constexpr int WF_FSHIFT = 27;
+constexpr uint32_t WF_PMASK = (1u << WF_FSHIFT) - 1u;
+constexpr int WF_CSTRIDE = 32;  // counters of one iteration: WF_SEGS x 128-byte lines
+
+// the view of segment s of a segmented queue
+__device__ __forceinline__ QueueArgs seg_view(const QueueArgs &Q, int s) {
+    QueueArgs V = Q;
+    V.cnt_out = Q.cnt_out + s * WF_CSTRIDE;
+    V.p_out = Q.p_out + s * Q.seg_cap;
+    V.d_out = Q.d_out + s * Q.seg_cap;
+    V.shade_cnt = Q.shade_cnt + s * WF_CSTRIDE;
+    V.shade_p = Q.shade_p + s * Q.seg_cap;
+    V.shade_d = Q.shade_d + s * Q.seg_cap;
+    return V;
+}
+
+// work unit u (of `per`-entry chunks over the segments' counts) -> segment, entry offset
+__device__ __forceinline__ bool seg_unit(const uint32_t *cnt, long u, int per, int &s, long &off, long &n_s) {
+    for (s = 0; s < WF_SEGS; ++s) {
+        n_s = cnt[s * WF_CSTRIDE];
+        const long units = (n_s + per - 1) / per;
+        if (u < units) { off = u * per; return true; }
+        u -= units;
+    }
+    return false;
+}
+__device__ __forceinline__ long seg_units(const uint32_t *cnt, int per) {
+    long U = 0;
+    for (int s = 0; s < WF_SEGS; ++s) U += ((long)cnt[s * WF_CSTRIDE] + per - 1) / per;
+    return U;
+}
+
+__global__ __launch_bounds__(256) void k_init_f(RenderArgs A, const FrameArgs *__restrict__ F, QueueArgs Q, long npix,
+                                                long total) {
+    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    bool hit = false;
+    float4 st_p = make_float4(0, 0, 0, 0), st_d = make_float4(0, 0, 0, 0);
+    if (t < total) {
+        const int f = (int)(t / npix);
+        const long px = t - (long)f * npix;
+        F[f].out[px] = 0u;
+        hit = gen_hit(A, F[f].inv_view, px, st_p, st_d);
+        st_d.w = __uint_as_float((uint32_t)px | ((uint32_t)f << WF_FSHIFT));
+    }
+    // seg_cap is a multiple of the block size: the block's pixels share a segment
+    const QueueArgs V = seg_view(Q, (int)(((long)blockIdx.x * blockDim.x) / Q.seg_cap));
+    const Slots sl = block_append2(hit, V.cnt_out, false, nullptr);
+    if (hit) { V.p_out[sl.a] = st_p; V.d_out[sl.a] = st_d; }
+}
+
+// One iteration over the queue: 64 rays per wave through mlp16 (4 x 16-point tiles, the
+// k_trace / k_mlp16 MLP), then the step and the block-aggregated compaction into the
+// ray's segment.  Blocks take 256-ray work units over the segments, grid-stride.
+template <int PREC>
+__global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueArgs Q, const FrameArgs *__restrict__ F,
+                                                 int it) {
+    Smem16 S = stage16(M, PREC);
+    const int wv = threadIdx.x >> 6;
+    const long U = seg_units(Q.cnt_in, 256);
+    for (long u = blockIdx.x; u < U; u += gridDim.x) {
+        int s;
+        long off, n_s;
+        seg_unit(Q.cnt_in, u, 256, s, off, n_s);
+        const long i = off + threadIdx.x;
+        const bool live = i < n_s;
+        float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
+        if (live) { sp = Q.p_in[s * Q.seg_cap + i]; sd = Q.d_in[s * Q.seg_cap + i]; }
+        const int f = live ? (int)(__float_as_uint(sd.w) >> WF_FSHIFT) : 0;
+        const long rem = n_s - (off + 64 * wv);
+        const uint32_t tmask = rem >= 64 ? 0xfu : (rem <= 0 ? 0u : (1u << ((rem + 15) >> 4)) - 1u);
+        float sdf = 0.0f;
+        if (tmask) sdf = mlp16(M, S.s32, S.slp, S.sfl, PREC, F[f].frame_f, sp.x, sp.y, sp.z, tmask);
+        march_rays(A, seg_view(Q, s), it, live, sp, sd, sdf, F[f].zoff);
+    }
+}
+
+// surfaceNormal + colour for the converged rays of the queue's frames: 16 rays x 4
+// tetrahedron points per wave, one fp32 4-tile mlp16 pass.
+__global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, QueueArgs Q, const FrameArgs *__restrict__ F) {
+    Smem16 S = stage16(M, NR_PRECISION_FP32);
+    const int lane = lane_id(), q = lane & 3;
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+    const long U = seg_units(Q.shade_cnt, 16);
+    for (long u = wave; u < U; u += nwaves) {
+        int s;
+        long off, n_s;
+        seg_unit(Q.shade_cnt, u, 16, s, off, n_s);
+        const long r = off + (lane >> 2);
+        const bool live = r < n_s;
+        float4 sp = make_float4(0, 0, 0, 0), sd = make_float4(0, 0, 0, 0);
+        if (live) { sp = Q.shade_p[s * Q.seg_cap + r]; sd = Q.shade_d[s * Q.seg_cap + r]; }
+        const uint32_t tag = __float_as_uint(sd.w);
+        const int f = live ? (int)(tag >> WF_FSHIFT) : 0;
+        const F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
+        const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
+        const long rem = n_s - off;  // rays; 4 per 16-point tile
+        const uint32_t tmask = rem >= 16 ? 0xfu : (1u << ((rem + 3) >> 2)) - 1u;
+        const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, F[f].frame_f, pq.x, pq.y, pq.z, tmask);
+        shade_rays(A, F[f].normal, F[f].out, F[f].zoff, live, sp, sd, tag & WF_PMASK, sdf);
     }
 }
 
@@ -737,6 +854,28 @@ hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float 
 }
 hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st) {
     hipLaunchKernelGGL(k_shade_l, dim3(grid), dim3(256), 0, st, Ad, Q, sdf4);
+    return hipGetLastError();
+}
+hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
+                         hipStream_t st) {
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_init_f, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, A, F, Q, npix, total);
+    return hipGetLastError();
+}
+hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
+                          int it, int grid, hipStream_t st) {
+    const int sm = smem_bytes(M, prec);
+    if (prec == NR_PRECISION_BF16)
+        hipLaunchKernelGGL(k_march16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (prec == NR_PRECISION_FP16)
+        hipLaunchKernelGGL(k_march16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else
+        hipLaunchKernelGGL(k_march16<NR_PRECISION_FP32>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    return hipGetLastError();
+}
+hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int grid,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_shade16, dim3(grid), dim3(256), smem_bytes(M, NR_PRECISION_FP32), st, A, M, Q, F);
     return hipGetLastError();
 }
 hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st) {

@@ -235,4 +235,33 @@ __device__ __forceinline__ uint32_t tiles_of(uint64_t m) {
            ((m >> 48) ? 8u : 0u);
 }
 
+// LDS staging of the 16-wide packs (dynamic shared memory, block-wide 16-byte copies)
+extern __shared__ __attribute__((aligned(16))) unsigned char nr_smem16[];
+
+struct Smem16 {
+    float *s32;       // fp32 16-wide pack
+    uint16_t *slp;    // bf16/fp16 A operands
+    float *sfl;       // float side of the low-precision pack
+};
+
+__device__ __forceinline__ Smem16 stage16(const MlpArgs &M, int prec) {
+    Smem16 S;
+    S.s32 = reinterpret_cast<float *>(nr_smem16);
+    S.slp = reinterpret_cast<uint16_t *>(nr_smem16 + M.pk_bytes);
+    S.sfl = reinterpret_cast<float *>(nr_smem16 + M.pk_bytes + M.lp_bytes);
+    const int4 *src = reinterpret_cast<const int4 *>(M.pk);
+    int4 *dst = reinterpret_cast<int4 *>(S.s32);
+    for (int i = threadIdx.x; i < M.pk_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    if (prec != NR_PRECISION_FP32) {
+        src = reinterpret_cast<const int4 *>(M.lp);
+        dst = reinterpret_cast<int4 *>(S.slp);
+        for (int i = threadIdx.x; i < M.lp_bytes / 16; i += blockDim.x) dst[i] = src[i];
+        src = reinterpret_cast<const int4 *>(M.lpf);
+        dst = reinterpret_cast<int4 *>(S.sfl);
+        for (int i = threadIdx.x; i < M.lpf_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
+    return S;
+}
+
 }  // namespace nr

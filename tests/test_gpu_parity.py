@@ -260,10 +260,12 @@ def test_iteration_map(rend, nets, chrome):
     assert ((m > 0) | (img == 0)).all()
 
 
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
 @pytest.mark.parametrize("nshards,shard,n", [(1, 0, 5), (3, 1, 3), (1, 0, 40)])
-def test_render_batch_matches_single_frames(rend, nets, chrome, nshards, shard, n):
-    """nr_render_batch: frames with their own cameras and frame numbers, in one launch
-    (40 frames: two launches), give each frame's single-frame pixels and summed stats."""
+def test_render_batch_matches_single_frames(rend, nets, chrome, nshards, shard, n, schedule):
+    """nr_render_batch: frames with their own cameras and frame numbers, in one launch /
+    one ray queue (40 frames: two), give each frame's single-frame pixels (persistent
+    schedule) and summed stats."""
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision("fp32").set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
     rend.set_matcap(chrome)
@@ -273,7 +275,9 @@ def test_render_batch_matches_single_frames(rend, nets, chrome, nshards, shard, 
         iv, nm = nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0)
         cams.append((iv, nm, int(rng.integers(0, 360))))
     W, H = 96, 77
+    rend.set_schedule(schedule)
     imgs, st = rend.render_batch(W, H, cams, 128, band=8, nshards=nshards, shard=shard)
+    rend.set_schedule("persistent")
     tot = 0
     for (iv, nm, fr), img in zip(cams, imgs):
         rend.set_view(iv, nm, fr)
@@ -284,7 +288,8 @@ def test_render_batch_matches_single_frames(rend, nets, chrome, nshards, shard, 
     rend.set_view(*nr.camera(0, 0, 2), 0)
 
 
-def test_render_batch_animation_vs_oracle(rend, nets, chrome):
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
+def test_render_batch_animation_vs_oracle(rend, nets, chrome, schedule):
     """A batch of an animation (the sphere grid moves with the frame number) equals the
     oracle frame by frame."""
     dims, K, B = nets["car_1"]
@@ -293,7 +298,26 @@ def test_render_batch_animation_vs_oracle(rend, nets, chrome):
     iv, nm = nr.camera(-15.0, 40.0, 2.0)
     cams = [(iv, nm, f) for f in (0, 90, 180)]
     W, H = 64, 64
+    rend.set_schedule(schedule)
     imgs, _ = rend.render_batch(W, H, cams, 128)
+    rend.set_schedule("persistent")
     for (iv_, nm_, f), img in zip(cams, imgs):
         ref, _ = oracle.OracleNet(K, B).render(W, H, iv_, nm_, frame=f, color_type=1, matcap=chrome, max_steps=128)
         assert np.array_equal(img, ref)
+
+
+def test_batch_after_buffer_growth(rend, nets, chrome):
+    """A batch, then a larger single frame (the ray queues grow), then the batch again:
+    the per-frame staging survives the queue reallocation."""
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
+    rend.set_matcap(chrome)
+    cams = [(*nr.camera(0.0, 30.0 * i, 2.0), i) for i in range(3)]
+    for schedule in ("persistent", "wavefront"):
+        rend.set_schedule(schedule)
+        a, _ = rend.render_batch(40, 30, cams, 64)
+        rend.set_view(*nr.camera(0, 0, 2), 0)
+        rend.render(1100 + (schedule == "wavefront") * 100, 1000, 16)
+        b, _ = rend.render_batch(40, 30, cams, 64)
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    rend.set_schedule("persistent")

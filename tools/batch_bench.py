@@ -16,14 +16,16 @@ ap.add_argument("--frames", type=int, default=64)
 ap.add_argument("--batches", default="1,4,16,32")
 ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--rays", type=int, default=64)
+ap.add_argument("--schedule", default="persistent")
+ap.add_argument("--shards", default="1,2,4,8")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 iv, nm = nr.camera(0, 0, 2)
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
-r.set_occupancy(a.bpc).set_wave_rays(a.rays)
+r.set_occupancy(a.bpc).set_wave_rays(a.rays).set_schedule(a.schedule)
 bufs = [torch.zeros(1024 * 1024, dtype=torch.int32, device="cuda") for _ in range(32)]
-for n in (1, 2, 4, 8):
+for n in (int(x) for x in a.shards.split(",")):
     line = []
     for b in (int(x) for x in a.batches.split(",")):
         cams = [(iv, nm, 0)] * b
@@ -37,4 +39,4 @@ for n in (1, 2, 4, 8):
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
         line.append(f"batch {b}: {dt:.3f} ms/frame")
-    print(f"n={n} bpc {a.bpc} rays {a.rays}: " + "  ".join(line), flush=True)
+    print(f"n={n} {a.schedule} bpc {a.bpc} rays {a.rays}: " + "  ".join(line), flush=True)
