@@ -20,8 +20,6 @@ r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(nr.load_png(nr
 r.set_schedule("wavefront").set_occupancy(a.bpc)
 bufs = [torch.zeros(1024 * 1024, dtype=torch.int32, device="cuda") for _ in range(a.batch)]
 for _ in range(a.reps):
-    st = r.render_batch_device([t.data_ptr() for t in bufs], 1024, 1024, [(iv, nm, 0)] * a.batch, 128, 8, 1, 0,
-                               with_stats=True) if False else None
     r.render_batch_device([t.data_ptr() for t in bufs], 1024, 1024, [(iv, nm, 0)] * a.batch, 128, 8, 1, 0)
 r.synchronize()
 print("done")
