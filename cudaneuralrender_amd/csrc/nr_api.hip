@@ -339,6 +339,7 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
     A.out = nullptr; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
     A.max_steps = max_steps; A.scene = c->scene; A.frame = 0; A.color_type = c->color_type;
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    set_recips(A);
     const int cus = num_cus(c->device);
     const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 16;  // measured: 4 -> 2.10, 8 -> 2.06, 16 -> 2.02 ms/frame (32-frame batch)
     uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + (size_t)(max_steps + 1) * line,
@@ -354,7 +355,7 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
         Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
         Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
         if ((rc = prof_begin(c, 0, s)) != NR_OK) return rc;
-        HIPCHK(c, launch_init_f(A, F, Q, (long)npix, (long)total, s));
+        HIPCHK(c, launch_init_f(A, F, Q, (long)npix, (long)total, cus * 8, s));
         if ((rc = prof_end(c, s)) != NR_OK) return rc;
         tot.launches += 2;
         const int grid = (int)std::max<size_t>(1, std::min<size_t>((total + 255) / 256, (size_t)cus * bpc));
@@ -799,6 +800,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     A.out = nullptr; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
     A.max_steps = max_steps; A.scene = c->scene; A.frame = 0; A.color_type = c->color_type;
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    set_recips(A);
     const size_t tr_bytes = NR_MAX_QUEUES * 128 + 4 * 8;
     if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
     TraceArgs T{};
@@ -901,6 +903,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     A.out = dout; A.W = W; A.H = H; A.rows = rows; A.band = band; A.nshards = nshards; A.shard = shard;
     A.max_steps = max_steps; A.scene = c->scene; A.frame = c->frame; A.color_type = c->color_type;
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
+    set_recips(A);
     memcpy(A.inv_view, c->inv_view, sizeof A.inv_view);
     memcpy(A.normal, c->normal, sizeof A.normal);
     GET_STREAM(c, s);

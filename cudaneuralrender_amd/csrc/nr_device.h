@@ -199,6 +199,16 @@ __device__ __forceinline__ int select_bit(uint64_t m, int d) {
     return lo;
 }
 
+// n / d (d >= 1) from a precomputed f64 reciprocal: n * (1/d) = (n/d)(1 + e), |e| <= 2^-52,
+// is within n/d * 2^-52 < 1/d of n/d -- closer than any non-integer n/d is to an
+// integer -- so the truncation is the quotient or, for an exact multiple, one less,
+// which the remainder test repairs.
+__device__ __forceinline__ uint32_t udiv_r(uint32_t n, uint32_t d, double inv_d) {
+    uint32_t q = (uint32_t)((double)n * inv_d);
+    if (n - q * d >= d) ++q;
+    return q;
+}
+
 // Exclusive position of this lane among the set lanes of `pred`, and one atomic per wave.
 __device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t *counter) {
     uint64_t m = __ballot(pred);

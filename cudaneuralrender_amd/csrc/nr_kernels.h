@@ -24,7 +24,12 @@ struct RenderArgs {
     int mw, mh;
     float inv_view[12];
     float normal[16];
+    double inv_w, inv_band;  // 1/W, 1/band for udiv_r (set_recips)
 };
+inline void set_recips(RenderArgs &A) {
+    A.inv_w = 1.0 / (double)A.W;
+    A.inv_band = 1.0 / (double)A.band;
+}
 
 // Ray queues: live rays {p.xyz, tfar} + {d.xyz, pixel}; converged rays {p.xyz, -} + {d.xyz, pixel}.
 struct QueueArgs {
@@ -97,7 +102,7 @@ hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long
 int dense_lds_bytes(int in, int out);
 hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
 hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
-                         hipStream_t st);
+                         int grid, hipStream_t st);
 hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
                           int it, int grid, hipStream_t st);
 hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int grid,

@@ -514,8 +514,9 @@ __global__ __launch_bounds__(256) void k_dense_col(DenseArgs D) {
 // initMarcher (:293-358) for pixel t of the shard, camera M (3x4): the ray's queue
 // entry {p, tfar}, {d, -} if it hits the bounding sphere.
 __device__ __forceinline__ bool gen_hit(const RenderArgs &A, const float *M, long t, float4 &st_p, float4 &st_d) {
-    int lr = (int)(t / A.W), x = (int)(t - (long)lr * A.W);
-    int y = ((lr / A.band) * A.nshards + A.shard) * A.band + (lr % A.band);
+    const int lr = (int)udiv_r((uint32_t)t, (uint32_t)A.W, A.inv_w), x = (int)t - lr * A.W;
+    const int bi = (int)udiv_r((uint32_t)lr, (uint32_t)A.band, A.inv_band);
+    const int y = (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
     F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
                dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
     float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
@@ -708,21 +709,25 @@ __device__ __forceinline__ long seg_units(const uint32_t *cnt, int per) {
 }
 
 __global__ __launch_bounds__(256) void k_init_f(RenderArgs A, const FrameArgs *__restrict__ F, QueueArgs Q, long npix,
-                                                long total) {
-    const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    bool hit = false;
-    float4 st_p = make_float4(0, 0, 0, 0), st_d = make_float4(0, 0, 0, 0);
-    if (t < total) {
-        const int f = (int)(t / npix);
-        const long px = t - (long)f * npix;
-        F[f].out[px] = 0u;
-        hit = gen_hit(A, F[f].inv_view, px, st_p, st_d);
-        st_d.w = __uint_as_float((uint32_t)px | ((uint32_t)f << WF_FSHIFT));
+                                                long total, double inv_npix) {
+    // grid-stride over 256-pixel chunks: a 32-frame batch has 131 k of them, and
+    // dispatching one workgroup per chunk cost ~1 ms
+    for (long c0 = (long)blockIdx.x * blockDim.x; c0 < total; c0 += (long)gridDim.x * blockDim.x) {
+        const long t = c0 + threadIdx.x;
+        bool hit = false;
+        float4 st_p = make_float4(0, 0, 0, 0), st_d = make_float4(0, 0, 0, 0);
+        if (t < total) {
+            const int f = (int)udiv_r((uint32_t)t, (uint32_t)npix, inv_npix);
+            const long px = t - (long)f * npix;
+            F[f].out[px] = 0u;
+            hit = gen_hit(A, F[f].inv_view, px, st_p, st_d);
+            st_d.w = __uint_as_float((uint32_t)px | ((uint32_t)f << WF_FSHIFT));
+        }
+        // seg_cap is a multiple of the block size: the chunk's pixels share a segment
+        const QueueArgs V = seg_view(Q, (int)(c0 / Q.seg_cap));
+        const Slots sl = block_append2(hit, V.cnt_out, false, nullptr);
+        if (hit) { V.p_out[sl.a] = st_p; V.d_out[sl.a] = st_d; }
     }
-    // seg_cap is a multiple of the block size: the block's pixels share a segment
-    const QueueArgs V = seg_view(Q, (int)(((long)blockIdx.x * blockDim.x) / Q.seg_cap));
-    const Slots sl = block_append2(hit, V.cnt_out, false, nullptr);
-    if (hit) { V.p_out[sl.a] = st_p; V.d_out[sl.a] = st_d; }
 }
 
 // One iteration over the queue: 64 rays per wave through mlp16 (4 x 16-point tiles, the
@@ -857,9 +862,10 @@ hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float 
     return hipGetLastError();
 }
 hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
-                         hipStream_t st) {
+                         int grid, hipStream_t st) {
     if (total <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_init_f, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, A, F, Q, npix, total);
+    grid = (int)std::max<long>(1, std::min<long>((total + 255) / 256, grid));
+    hipLaunchKernelGGL(k_init_f, dim3(grid), dim3(256), 0, st, A, F, Q, npix, total, 1.0 / (double)npix);
     return hipGetLastError();
 }
 hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,

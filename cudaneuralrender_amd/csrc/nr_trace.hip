@@ -23,15 +23,6 @@ namespace nr {
 
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
-// n / d (d >= 1) from a precomputed f64 reciprocal: n * (1/d) = (n/d)(1 + e), |e| <= 2^-52,
-// is within n/d * 2^-52 < 1/d of n/d -- closer than any non-integer n/d is to an
-// integer -- so the truncation is the quotient or, for an exact multiple, one less,
-// which the remainder test repairs.
-__device__ __forceinline__ uint32_t udiv_r(uint32_t n, uint32_t d, double inv_d) {
-    uint32_t q = (uint32_t)((double)n * inv_d);
-    if (n - q * d >= d) ++q;
-    return q;
-}
 
 // Ray generation for pixel x of local row lr of the shard (initMarcher :293-358).
 // Returns hit.
