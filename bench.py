@@ -13,8 +13,9 @@ longest rays march while the next frame's pixels keep the matrix cores busy -- e
 frame is rendered in full, none is reused.  config.single_frame repeats the timing with
 one nr_render call per frame (each launch waits for the previous frame's last ray).
 
-N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt in 8-row bands
-round-robin (nr_render_batch's shard arguments), each rank renders its bands of every
+N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt round-robin one
+row at a time (band 1, nr_render_batch's shard arguments: the slowest of 8 ranks is within
+1% of the mean, against 6% for 8-row bands -- tools/shard_balance.py), each rank renders its rows of every
 frame, then one RCCL gather (torch.distributed.gather over the "nccl" backend) brings
 the batch's shards to rank 0 -- one collective for the K frames, single-frame timing:
 one per frame -- which re-interleaves each frame (nr_assemble_shards).  The frame size
@@ -38,7 +39,7 @@ sys.path.insert(0, REPO)
 FLOP_PER_EVAL = 2 * (3 * 32 + 7 * 32 * 32 + 32 * 1)   # 14,592
 PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}  # TFLOP/s dense, MI355X_MICROARCH.md
 MAX_STEPS = 128
-BAND = 8
+BAND = 1  # rows per band dealt round-robin to the ranks (profiles/r1_shard_balance.txt)
 MAX_BATCH = 32  # frames per k_trace launch (NR_MAX_BATCH)
 
 
