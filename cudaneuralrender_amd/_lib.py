@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libnr.so")
+# NR_LIBRARY: an alternative build of the same ABI (A/B experiments under tools/)
+LIB_PATH = os.environ.get("NR_LIBRARY") or os.path.join(_HERE, "lib", "libnr.so")
 
 NR_OK = 0
 NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}

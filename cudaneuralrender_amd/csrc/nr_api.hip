@@ -40,11 +40,10 @@ struct nr_ctx {
     std::vector<float *> d_W, d_b;                     // out-major per layer (generic kernel)
     bool fused = false;
     int precision = NR_PRECISION_FP32;
-    float *d_pack32 = nullptr, *d_pack16 = nullptr;
-    uint16_t *d_lp = nullptr, *d_lp16 = nullptr;
-    float *d_lpf = nullptr, *d_lpf16 = nullptr;
-    MlpArgs mlp{};    // 32-point tiles: k_mlp, k_march, k_shade (wavefront schedule)
-    MlpArgs mlp16{};  // 16-point tiles: k_trace, k_shade16 (persistent schedule)
+    float *d_pack16 = nullptr;
+    uint16_t *d_lp16 = nullptr;
+    float *d_lpf16 = nullptr;
+    MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
     int debug = 0;
@@ -136,7 +135,6 @@ int free_network(nr_ctx *c) {
     for (auto *p : c->d_W) (void)hipFree(p);
     for (auto *p : c->d_b) (void)hipFree(p);
     c->d_W.clear(); c->d_b.clear();
-    dfree(c->d_pack32); dfree(c->d_lp); dfree(c->d_lpf);
     dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16);
     c->fused = false;
     if (c->lgraph) { (void)hipGraphExecDestroy(c->lgraph); c->lgraph = nullptr; }
@@ -161,15 +159,11 @@ int upload_pack(nr_ctx *c, const std::vector<uint16_t> &a, const std::vector<flo
 }
 
 int upload_lowp(nr_ctx *c) {
-    dfree(c->d_lp); dfree(c->d_lpf); dfree(c->d_lp16); dfree(c->d_lpf16);
-    for (MlpArgs *M : {&c->mlp, &c->mlp16}) { M->lp = nullptr; M->lpf = nullptr; M->lp_bytes = 0; M->lpf_bytes = 0; }
+    dfree(c->d_lp16); dfree(c->d_lpf16);
+    c->mlp16.lp = nullptr; c->mlp16.lpf = nullptr; c->mlp16.lp_bytes = 0; c->mlp16.lpf_bytes = 0;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
-    if (!pack_lowp(c->dims, c->kernels, c->biases, c->precision, a, f))
-        return set_err(c, NR_E_INVALID, "low-precision pack failed");
-    int rc = upload_pack(c, a, f, c->d_lp, c->d_lpf, c->mlp);
-    if (rc != NR_OK) return rc;
     if (!pack_lowp_16(c->dims, c->kernels, c->biases, c->precision, a, f))
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
     return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
@@ -193,24 +187,18 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
         HIPCHK(c, hipMemcpy(dw, W.data(), W.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(db, c->biases[l].data(), (size_t)out * 4, hipMemcpyHostToDevice));
     }
-    std::vector<float> pack, pack16;
-    c->fused = pack_fp32(c->dims, c->kernels, c->biases, pack) &&
-               pack_fp32_16(c->dims, c->kernels, c->biases, pack16);
-    c->mlp = MlpArgs{};
+    std::vector<float> pack16;
+    c->fused = pack_fp32_16(c->dims, c->kernels, c->biases, pack16);
     c->mlp16 = MlpArgs{};
     if (c->fused) {
-        size_t pb = (pack.size() * 4 + 15) / 16 * 16;
-        pack.resize(pb / 4, 0.0f);
+        size_t pb = (pack16.size() * 4 + 15) / 16 * 16;
         pack16.resize(pb / 4, 0.0f);
-        HIPCHK(c, hipMalloc(&c->d_pack32, pb));
-        HIPCHK(c, hipMemcpy(c->d_pack32, pack.data(), pb, hipMemcpyHostToDevice));
         HIPCHK(c, hipMalloc(&c->d_pack16, pb));
         HIPCHK(c, hipMemcpy(c->d_pack16, pack16.data(), pb, hipMemcpyHostToDevice));
-        c->mlp.pk = c->d_pack32;
         c->mlp16.pk = c->d_pack16;
-        c->mlp.pk_bytes = c->mlp16.pk_bytes = (int)pb;
-        c->mlp.in0 = c->mlp16.in0 = c->dims[0];
-        c->mlp.nh = c->mlp16.nh = nl - 2;
+        c->mlp16.pk_bytes = (int)pb;
+        c->mlp16.in0 = c->dims[0];
+        c->mlp16.nh = nl - 2;
     }
     return upload_lowp(c);
 }
@@ -746,7 +734,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (W < 1 || H < 1 || (long)W * H > (1l << 31)) return set_err(c, NR_E_INVALID, "nr_render: bad size %dx%d", W, H);
     if (band < 1 || nshards < 1 || shard < 0 || shard >= nshards) return set_err(c, NR_E_INVALID, "nr_render: bad shard");
     if (max_steps < 0) return set_err(c, NR_E_INVALID, "nr_render: max_steps < 0");
-    if (c->schedule == NR_SCHED_WAVEFRONT && c->fused && !(c->debug & 2)) {
+    if (c->schedule == NR_SCHED_WAVEFRONT && c->fused) {
         if (c->dims[0] != c->num_inputs)
             return set_err(c, NR_E_STATE, "nr_render: network takes %d inputs but numInputs = %d", c->dims[0], c->num_inputs);
         if (c->color_type == NR_COLOR_MATCAP && !c->d_matcap) return set_err(c, NR_E_STATE, "nr_render: matcap colouring without a matcap");
@@ -754,7 +742,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         GET_STREAM(c, s);
         return render_wavefront(c, frames, nframes, W, H, band, nshards, shard, max_steps, loc, stats, s);
     }
-    if (c->schedule != NR_SCHED_PERSISTENT || !c->fused || (c->debug & (1 | 2 | 8))) {
+    if (c->schedule != NR_SCHED_PERSISTENT || !c->fused || (c->debug & (1 | 8))) {
         // frame by frame (the wavefront and layered schedules and the diagnostics are
         // single-frame)
         float iv[12], nm[16];
@@ -1014,59 +1002,19 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         }
         return NR_OK;
     }
-    if (!(c->debug & 2)) {
-        // ---- wavefront schedule (16-point tiles, render_wavefront) on this one frame
-        nr_frame fr{};
-        memcpy(fr.inv_view, c->inv_view, sizeof fr.inv_view);
-        memcpy(fr.normal, c->normal, sizeof fr.normal);
-        fr.frame = c->frame;
-        fr.out = dout;
-        if ((rc2 = render_wavefront(c, &fr, 1, W, H, band, nshards, shard, max_steps, NR_DEVICE, stats, s)) != NR_OK)
-            return rc2;
-        if (loc != NR_DEVICE) {
-            HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-        }
-        return NR_OK;
+    // ---- wavefront schedule (render_wavefront) on this one frame
+    nr_frame fr{};
+    memcpy(fr.inv_view, c->inv_view, sizeof fr.inv_view);
+    memcpy(fr.normal, c->normal, sizeof fr.normal);
+    fr.frame = c->frame;
+    fr.out = dout;
+    if ((rc2 = render_wavefront(c, &fr, 1, W, H, band, nshards, shard, max_steps, NR_DEVICE, stats, s)) != NR_OK)
+        return rc2;
+    if (loc != NR_DEVICE) {
+        HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
     }
-    // ---- debug bit 1: the 32-point-tile wavefront kernels (k_march / k_shade), kept for comparison
-    // counters: [0, max_steps] live counts, [max_steps+1] shade count, [max_steps+2 ...] shade_it
-    uint32_t *cnt = c->d_ctr, *shade_cnt = c->d_ctr + max_steps + 1, *shade_it = c->d_ctr + max_steps + 2;
-    size_t nctr = (size_t)2 * max_steps + 2;
-    HIPCHK(c, hipEventRecord(c->ev0, s));
-    HIPCHK(c, hipMemsetAsync(c->d_ctr, 0, nctr * 4, s));
-    QueueArgs Q{};
-    Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
-    Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
-    if ((rc2 = prof_begin(c, 0, s)) != NR_OK) return rc2;
-    HIPCHK(c, launch_init(A, Q, s));
-    if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
-    int launches = 2;
-    int march_grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * 4);
-    if (march_grid < 1) march_grid = 1;
-    for (int it = 0; it < max_steps; ++it) {
-        Q.cnt_in = cnt + it; Q.cnt_out = cnt + it + 1;
-        Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
-        Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
-        if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
-        HIPCHK(c, launch_march(A, c->mlp, Q, c->precision, it, march_grid, s));
-        if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
-        ++launches;
-        if (c->check_every > 0 && (it + 1) % c->check_every == 0 && it + 1 < max_steps) {
-            HIPCHK(c, hipMemcpyAsync(c->h_ctr, cnt + it + 1, 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            if (c->h_ctr[0] == 0) break;
-        }
-    }
-    int shade_grid = (int)std::min<size_t>((npix + 1023) / 1024, (size_t)cus * 4);
-    if (shade_grid < 1) shade_grid = 1;
-    if ((rc2 = prof_begin(c, 2, s)) != NR_OK) return rc2;
-    HIPCHK(c, launch_shade(A, c->mlp, Q, shade_grid, s));
-    if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
-    if (c->profiling) c->prof_renders++;
-    HIPCHK(c, hipEventRecord(c->ev1, s));
-    if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
-    return queue_stats(c, max_steps, launches, stats, s);
+    return NR_OK;
 }
 
 int nr_render(nr_ctx *c, uint32_t *out, int W, int H, int max_steps, int loc, nr_stats *stats) {
@@ -1117,10 +1065,8 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
-        else if ((c->debug & 2) == 0)
+        else
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
-        else  // 32-point-tile variant (k_mlp), kept for comparison
-            HIPCHK(c, launch_mlp(c->mlp, c->precision, dX, dY, n, std::max(grid, 1), s));
     } else {
         float *bufs[2] = {scratch, scratch + (size_t)chunk * maxw};
         const int cus = num_cus(c->device);

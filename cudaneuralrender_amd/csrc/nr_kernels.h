@@ -98,7 +98,6 @@ struct TraceArgs {
 };
 
 int smem_bytes(const MlpArgs &M, int prec);
-hipError_t launch_mlp(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
 int dense_lds_bytes(int in, int out);
 hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
 hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
@@ -111,10 +110,6 @@ hipError_t launch_set_args(const RenderArgs &A, RenderArgs *d, hipStream_t st);
 hipError_t launch_init_l(const RenderArgs *Ad, const QueueArgs &Q, long npix, hipStream_t st);
 hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf, int it, int grid, hipStream_t st);
 hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st);
-hipError_t launch_init(const RenderArgs &A, const QueueArgs &Q, hipStream_t st);
-hipError_t launch_march(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int prec, int it, int grid,
-                        hipStream_t st);
-hipError_t launch_shade(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
 hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, int part, hipStream_t st);

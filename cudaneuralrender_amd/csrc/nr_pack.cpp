@@ -3,8 +3,8 @@
 // Input: Keras Dense kernels (in x out, row-major) as HighFive hands them to the
 // DenseLayer constructor (reference src/layers/denseLayer.cu:180-227, which
 // transposes them to out-major W[out][in]).  Output: register-layout-ready packs
-// for the kernels in nr_kernels.hip (layout documented in nr_internal.h and
-// DESIGN.md "MLP on MFMA").
+// for the 16-point-tile MLP (nr_mlp16.h; layout documented in nr_internal.h and
+// DESIGN.md §4).
 #include "nr_internal.h"
 
 #include <cmath>
@@ -21,13 +21,6 @@ bool fused_shape_ok(const std::vector<int> &dims) {
 }
 
 namespace {
-// physical accumulator row of (lane half h, register r) for a 32x32 MFMA tile
-inline int acc_row(int h, int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-// hidden unit held by (half h, register r) in the fp32 path: consumer = next MFMA
-// layer -> interleaved (2r + h) so that the f32 MFMA k-order is ascending; consumer
-// = final VALU layer -> halves (16h + r) so one cross-lane hand-off suffices.
-inline int unit_f32(int h, int r, bool final_consumer) { return final_consumer ? 16 * h + r : 2 * r + h; }
-
 uint16_t f2bf16(float x) {
     uint32_t u; memcpy(&u, &x, 4);
     if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
@@ -53,77 +46,6 @@ uint16_t f2fp16(float x) {
     return (uint16_t)(sign | (uint32_t)exp << 10 | (uint32_t)mant);
 }
 }  // namespace
-
-bool pack_fp32(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-               const std::vector<std::vector<float>> &B, std::vector<float> &pack) {
-    if (!fused_shape_ok(dims)) return false;
-    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
-    pack.assign(pk_floats(nh), 0.0f);
-    // layer 0 (VALU): K[0] is (in0 x 32)
-    for (int h = 0; h < 2; ++h)
-        for (int r = 0; r < 16; ++r) {
-            int u = unit_f32(h, r, nh == 0);
-            for (int k = 0; k < 4; ++k)
-                pack[PK_L0W + (h * 16 + r) * 4 + k] = (k < in0) ? K[0][(size_t)k * 32 + u] : 0.0f;
-            pack[PK_L0B + h * 16 + r] = B[0][u];
-        }
-    // hidden 32x32 layers on v_mfma_f32_32x32x2_f32
-    for (int j = 0; j < nh; ++j) {
-        const std::vector<float> &Kj = K[j + 1];
-        bool fin = (j == nh - 1);
-        int base = PK_HID + j * PK_HID_STRIDE;
-        for (int s = 0; s < 16; ++s)
-            for (int lane = 0; lane < 64; ++lane) {
-                int i = lane & 31, kk = lane >> 5;
-                int hi = (i >> 2) & 1, si = (i & 3) + 4 * (i >> 3);
-                int uout = fin ? 16 * hi + si : 2 * si + hi;
-                int uin = 2 * s + kk;
-                pack[base + ((s >> 2) * 64 + lane) * 4 + (s & 3)] = Kj[(size_t)uin * 32 + uout];
-            }
-        for (int h = 0; h < 2; ++h)
-            for (int r = 0; r < 16; ++r) pack[base + 1024 + h * 16 + r] = B[j + 1][unit_f32(h, r, fin)];
-    }
-    // final 32 -> 1 (VALU): half h register r holds unit 16h + r (or 2r + h when nh == 0... see below)
-    int fo = pk_final(nh);
-    for (int h = 0; h < 2; ++h)
-        for (int r = 0; r < 16; ++r) pack[fo + h * 16 + r] = K[nl - 1][16 * h + r];
-    pack[fo + 32] = B[nl - 1][0];
-    return true;
-}
-
-bool pack_lowp(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-               const std::vector<std::vector<float>> &B, int precision, std::vector<uint16_t> &a_ops,
-               std::vector<float> &fl) {
-    if (!fused_shape_ok(dims)) return false;
-    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
-    auto cvt = [&](float v) { return precision == NR_PRECISION_BF16 ? f2bf16(v) : f2fp16(v); };
-    a_ops.assign((size_t)nh * LP_A_ELEMS, 0);
-    // float side: [L0W 128][L0B 32][hidden bias 32 x nh][final w 32][final b 1 + 3 pad]
-    fl.assign(160 + 32 * nh + 36, 0.0f);
-    for (int h = 0; h < 2; ++h)
-        for (int r = 0; r < 16; ++r) {
-            int u = acc_row(h, r);
-            for (int k = 0; k < 4; ++k) fl[(h * 16 + r) * 4 + k] = (k < in0) ? K[0][(size_t)k * 32 + u] : 0.0f;
-            fl[128 + h * 16 + r] = B[0][u];
-        }
-    for (int j = 0; j < nh; ++j) {
-        const std::vector<float> &Kj = K[j + 1];
-        for (int ks = 0; ks < 2; ++ks)
-            for (int lane = 0; lane < 64; ++lane)
-                for (int e = 0; e < 8; ++e) {
-                    int i = lane & 31, hh = lane >> 5;
-                    int uin = 16 * ks + 8 * (e >> 2) + 4 * hh + (e & 3);
-                    a_ops[(size_t)j * LP_A_ELEMS + (ks * 64 + lane) * 8 + e] = cvt(Kj[(size_t)uin * 32 + i]);
-                }
-        for (int h = 0; h < 2; ++h)
-            for (int r = 0; r < 16; ++r) fl[160 + 32 * j + h * 16 + r] = B[j + 1][acc_row(h, r)];
-    }
-    int fo = 160 + 32 * nh;
-    for (int h = 0; h < 2; ++h)
-        for (int r = 0; r < 16; ++r) fl[fo + h * 16 + r] = K[nl - 1][acc_row(h, r)];
-    fl[fo + 32] = B[nl - 1][0];
-    return true;
-}
 
 // ---- 16-point tiles (nr_mlp16.h).  Lane (j, g): point j, unit group g; register k.
 namespace {

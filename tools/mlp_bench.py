@@ -21,7 +21,6 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1 << 22)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--precision", default="all")
-ap.add_argument("--variant", default="16")
 ap.add_argument("--bpc", default="4")
 a = ap.parse_args()
 X = np.random.default_rng(0).uniform(-1, 1, size=(a.n, 3)).astype(np.float32)
@@ -31,11 +30,9 @@ r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
 res = []
 for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else [a.precision]):
-    for variant, bpc in [(v, int(b)) for v in (["16", "32"] if a.variant == "all" else [a.variant])
-                         for b in a.bpc.split(",")]:
+    for bpc in (int(b) for b in a.bpc.split(",")):
         r.set_occupancy(bpc)
         r.set_precision(prec)
-        r.set_debug(0 if variant == "16" else 2)
         for _ in range(3):
             r.mlp_forward_device(dX.data_ptr(), dY.data_ptr(), a.n)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -47,6 +44,6 @@ for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else [a.precision]
         ms = e0.elapsed_time(e1) / a.iters
         tf = a.n * 14592 / (ms * 1e-3) / 1e12
         util = a.n * 14336 / (ms * 1e-3) / 1e12 / PEAK[prec]
-        res.append({"precision": prec, "tile": variant, "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
+        res.append({"precision": prec, "tile": "16", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
                     "hidden_layer_mfma_util": round(util, 4), "Gpoints_per_s": round(a.n / ms / 1e6, 2)})
         print(json.dumps(res[-1]), flush=True)
