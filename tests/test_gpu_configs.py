@@ -109,3 +109,21 @@ def test_c5_geometries_fp16_2048(rend, nets, chrome, geom):
         rend.set_precision("fp32")
     assert iou(h, f) > 0.97
     assert abs(sh["ray_steps"] - sf["ray_steps"]) / max(sf["ray_steps"], 1) < 0.10
+
+
+def test_large_frame_8192(rend, nets, chrome):
+    """An 8192^2 frame (64 Mpixel, beyond the configs): the persistent and wavefront
+    schedules agree pixel for pixel and in every count, and the 3 row-band shards of
+    one rank layout re-assemble to it (size-independent properties; the oracle would
+    need minutes)."""
+    setup(rend, nets, "plane_1", "fp32", chrome, cam=(-10.0, 25.0, 2.0))
+    N = 8192
+    a, sa = rend.set_schedule("persistent").render(N, N, 12)
+    b, sb = rend.set_schedule("wavefront").render(N, N, 12)
+    rend.set_schedule("persistent")
+    assert sa["rays_hit"] > N * N // 4
+    for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
+        assert sa[k] == sb[k], (k, sa, sb)
+    assert np.array_equal(a, b)
+    shards = [rend.render_shard(N, N, 1, 3, s, 12)[0] for s in range(3)]
+    assert np.array_equal(nr.assemble_shards(shards, N, N, 1, 3), a)

@@ -47,3 +47,22 @@ def test_renderer_single_png(tmp_path, matcap, scene):
     assert np.array_equal(png, ref[::-1, ::-1])
     ppm = open(str(tmp_path / "plane_1.h5.png.ppm"), "rb").read()
     assert ppm.startswith(b"P6\n96\n80\n255\n")
+
+
+def test_renderer_spin(tmp_path):
+    """--spin (doABarrelRoll, main.cpp:470-478): 360 frames, rotY = frame number = i,
+    saved as 000.png ... 359.png (main.cpp:445-458 naming)."""
+    args = [os.path.join(BIN, "neuralSDFRenderer"), "-i", nr.geometry_path("car_1"), "-o", str(tmp_path) + "/",
+            "-W", "24", "-H", "20", "-rx", "-15", "--spin", "--max-steps", "96", "-M", nr.matcap_path("Chrome")]
+    p = run(args)
+    assert p.returncode == 0, p.stdout + p.stderr
+    names = sorted(os.listdir(tmp_path))
+    assert len(names) == 360 and names[0] == "000.png" and names[-1] == "359.png"
+    dims, K, B = nr.read_keras_h5(nr.geometry_path("car_1"))
+    mc = nr.load_png(nr.matcap_path("Chrome"))
+    net = oracle.OracleNet(K, B)
+    for i in (0, 45, 200, 359):
+        iv, nm = nr.camera(-15, float(i), 2.0)
+        ref, _ = net.render(24, 20, iv, nm, frame=i, color_type=1, matcap=mc, max_steps=96)
+        png = nr.load_png(str(tmp_path / f"{i:03d}.png"))
+        assert np.array_equal(png, ref[::-1, ::-1]), i
