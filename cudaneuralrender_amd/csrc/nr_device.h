@@ -45,6 +45,26 @@ __device__ __forceinline__ int f2i_rz(float f) {
     return (int)f;
 }
 
+// intersectSphere (volumeRender_kernel.cu:199-215) against the bounding sphere (c = 0,
+// r = 1.2).  The reference forms b as (float)(2.0 * (double)dot) -- exact in f32 -- and
+// each root as an f64 division rounded to f32; a single correctly rounded f32 division
+// gives the same bits (innocuous double rounding: 53 >= 2*24 + 2), proven on the CPU by
+// tests/test_oracle.py::test_intersect_sphere_f32_division_bit_exact.  Saves the two
+// f64 divisions per generated ray.
+__device__ __forceinline__ bool intersect_bounding(F3 o, F3 d, float &tnear, float &tfar) {
+    const F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
+    const float a = dot3(d, d);
+    const float b = 2.0f * dot3(Qv, d);
+    const float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
+    const float disc = b * b - 4 * a * cc;
+    if (!(disc > 0)) return false;
+    const float sq = sqrtf(disc);
+    const float a2 = 2.0f * a;
+    tnear = (-b - sq) / a2;
+    tfar = (-b + sq) / a2;
+    return true;
+}
+
 static __constant__ float c_tet[12] = {1, -1, -1, -1, -1, 1, -1, 1, -1, 1, 1, 1};  // :38-43
 #define NORMAL_EPSILON 0.00001f
 #define MARCHING_EPSILON 0.000001f

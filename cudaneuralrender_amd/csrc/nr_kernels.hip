@@ -325,15 +325,8 @@ __device__ __forceinline__ bool gen_hit(const RenderArgs &A, const float *M, lon
     F3 d = normalize3(mk3(u, v, -2.0f));
     d = mk3(dot3(d, mk3(M[0], M[1], M[2])), dot3(d, mk3(M[4], M[5], M[6])), dot3(d, mk3(M[8], M[9], M[10])));
     // intersectSphere (:199-215), bounding sphere c = 0, r = 1.2
-    F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
-    float a = dot3(d, d);
-    float b = (float)(2.0 * (double)dot3(Qv, d));
-    float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
-    float disc = b * b - 4 * a * cc;
-    if (!(disc > 0)) return false;
-    float sq = sqrtf(disc);
-    float tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
-    float tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
+    float tnear, tfar;
+    if (!intersect_bounding(o, d, tnear, tfar)) return false;
     if (tnear < 0.0f) tnear = 0.0f;
     F3 p = add3(o, mul3s(d, tnear));
     st_p = make_float4(p.x, p.y, p.z, tfar);

@@ -39,15 +39,8 @@ __device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T,
     float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
     F3 dd = normalize3(mk3(u, v, -2.0f));
     dd = mk3(dot3(dd, mk3(M[0], M[1], M[2])), dot3(dd, mk3(M[4], M[5], M[6])), dot3(dd, mk3(M[8], M[9], M[10])));
-    F3 Qv = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
-    float a = dot3(dd, dd);
-    float b = (float)(2.0 * (double)dot3(Qv, dd));
-    float cc = dot3(Qv, Qv) - 1.2f * 1.2f;
-    float disc = b * b - 4 * a * cc;
-    if (!(disc > 0)) return false;
-    float sq = sqrtf(disc);
-    float tnear = (float)((double)(-b - sq) / (2.0 * (double)a));
-    tfar = (float)((double)(-b + sq) / (2.0 * (double)a));
+    float tnear;
+    if (!intersect_bounding(o, dd, tnear, tfar)) return false;
     if (tnear < 0.0f) tnear = 0.0f;
     p = add3(o, mul3s(dd, tnear));
     d = dd;

@@ -554,7 +554,42 @@ float or_many_sphere_ref(float px, float py, float pz, float nsdf, int frame)
     return manySphere(mk3(px, py, pz), nsdf, frame);
 }
 
+/* intersectSphere as the kernels evaluate it (nr_trace.hip gen_ray, nr_kernels.hip
+ * k_init_f): b = 2*dot in f32 (the f64 product of a float by 2 is exact), and each root
+ * as ONE correctly rounded f32 division.  The reference divides in f64 and rounds to
+ * f32; for a quotient of two floats that double rounding is innocuous (53 >= 2*24 + 2,
+ * Figueroa 1995), so the two forms agree bit for bit. */
+static int intersect_kernelform(f3 o, f3 d, float r, float *tnear, float *tfar)
+{
+    f3 Q = mk3(o.x - 0.0f, o.y - 0.0f, o.z - 0.0f);
+    float a = dot3(d, d);
+    float b = 2.0f * dot3(Q, d);
+    float c = dot3(Q, Q) - r * r;
+    float discrim = b * b - 4 * a * c;
+    if (discrim > 0) {
+        float sq = sqrtf(discrim);
+        float a2 = 2.0f * a;
+        *tnear = (-b - sq) / a2;
+        *tfar = (-b + sq) / a2;
+        return 1;
+    }
+    return 0;
+}
+
 /* Batch helpers for the equivalence tests: out[i] = f(in...). */
+void or_batch_intersect(const float *o, const float *d, long n, float r, float *ref, float *ker)
+{
+    for (long i = 0; i < n; ++i) {
+        f3 oo = mk3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), dd = mk3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        float tn = 0.0f, tf = 0.0f;
+        int h = intersectSphere(oo, dd, r, &tn, &tf);
+        ref[3 * i] = (float)h; ref[3 * i + 1] = h ? tn : 0.0f; ref[3 * i + 2] = h ? tf : 0.0f;
+        tn = tf = 0.0f;
+        h = intersect_kernelform(oo, dd, r, &tn, &tf);
+        ker[3 * i] = (float)h; ker[3 * i + 1] = h ? tn : 0.0f; ker[3 * i + 2] = h ? tf : 0.0f;
+    }
+}
+
 void or_batch_smooth_union(const float *d1, const float *d2, long n, float k, float *ref, float *ker)
 {
     for (long i = 0; i < n; ++i) {

@@ -40,6 +40,8 @@ def lib():
         L.or_batch_smooth_union.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
         L.or_batch_many_sphere.restype = None
         L.or_batch_many_sphere.argtypes = [P, P, ctypes.c_long, I, P, P]
+        L.or_batch_intersect.restype = None
+        L.or_batch_intersect.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
         _lib = L
     return _lib
 
@@ -114,4 +116,14 @@ def many_sphere_pair(p, nsdf, frame=0):
     ref = np.zeros_like(nsdf)
     ker = np.zeros_like(nsdf)
     lib().or_batch_many_sphere(p.ctypes.data, nsdf.ctypes.data, nsdf.size, frame, ref.ctypes.data, ker.ctypes.data)
+    return ref, ker
+
+
+def intersect_pair(o, d, r=1.2):
+    """(reference form, kernel form) of intersectSphere: [hit, tnear, tfar] per ray."""
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    ref = np.zeros_like(o)
+    ker = np.zeros_like(o)
+    lib().or_batch_intersect(o.ctypes.data, d.ctypes.data, o.shape[0], r, ref.ctypes.data, ker.ctypes.data)
     return ref, ker

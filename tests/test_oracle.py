@@ -152,3 +152,30 @@ def test_many_sphere_far_test_bit_exact(frame):
     p = (centre + dirs * rad[:, None]).astype(np.float32)
     ref, ker = oracle.many_sphere_pair(p, s, frame)
     assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
+
+
+def test_intersect_sphere_f32_division_bit_exact():
+    """The kernels' ray generation (nr_trace.hip gen_ray, nr_kernels.hip k_init_f) takes
+    each root of intersectSphere (volumeRender_kernel.cu:199-215) as one f32 division
+    where the reference divides in f64 and rounds: innocuous double rounding (53 >= 2*24+2)
+    makes them bit-identical.  Checked on eye rays of random cameras (the renderer's
+    distribution), on random origins/directions over many magnitudes, and on edge cases."""
+    rng = np.random.default_rng(11)
+    n = 2_000_000
+    # camera-like rays: origin at distance ~zoom, unit-ish directions through the sphere
+    zoom = rng.uniform(0.5, 6.0, n)
+    o = rng.standard_normal((n, 3))
+    o *= (zoom / np.linalg.norm(o, axis=1))[:, None]
+    d = -o / zoom[:, None] + rng.normal(0, 0.4, (n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    # arbitrary magnitudes (denormal-ish to huge), unnormalised directions
+    m = n // 2
+    o2 = rng.standard_normal((m, 3)) * 10.0 ** rng.uniform(-20, 18, (m, 1))
+    d2 = rng.standard_normal((m, 3)) * 10.0 ** rng.uniform(-20, 18, (m, 1))
+    edge_o = np.array([[0, 0, 2], [0, 0, 1.2], [0, 0, 0], [1.2, 0, 0], [0, 0, -2], [1e30, 0, 0], [0, 1.2, 1e-30]])
+    edge_d = np.array([[0, 0, -1], [0, 0, -1], [0, 0, 1], [0, 1, 0], [0, 0, 0], [-1, 0, 0], [0, -1e-20, 0]])
+    O = np.concatenate([o, o2, edge_o]).astype(np.float32)
+    D = np.concatenate([d, d2, edge_d]).astype(np.float32)
+    ref, ker = oracle.intersect_pair(O, D, 1.2)
+    assert ref[:, 0].sum() > n // 2  # most camera rays hit
+    assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
