@@ -21,6 +21,11 @@
 
 namespace nr {
 
+// workgroups per CU the register allocation of k_trace targets (4 waves each)
+#ifndef NR_TRACE_BPC
+#define NR_TRACE_BPC 3
+#endif
+
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
 
@@ -69,7 +74,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // frame-dependent values (camera, sphere offset, animation input, output image) come
 // from the FrameArgs staged in LDS.
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
-__global__ __launch_bounds__(256, 3) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {

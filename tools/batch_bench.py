@@ -18,25 +18,29 @@ ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--rays", type=int, default=64)
 ap.add_argument("--schedule", default="persistent")
 ap.add_argument("--shards", default="1,2,4,8")
+ap.add_argument("--precision", default="fp32")
+ap.add_argument("--size", type=int, default=1024)
+ap.add_argument("--steps", type=int, default=128)
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 iv, nm = nr.camera(0, 0, 2)
-r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
+r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
 r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
 r.set_occupancy(a.bpc).set_wave_rays(a.rays).set_schedule(a.schedule)
-bufs = [torch.zeros(1024 * 1024, dtype=torch.int32, device="cuda") for _ in range(32)]
+S = a.size
+bufs = [torch.zeros(S * S, dtype=torch.int32, device="cuda") for _ in range(32)]
 for n in (int(x) for x in a.shards.split(",")):
     line = []
     for b in (int(x) for x in a.batches.split(",")):
         cams = [(iv, nm, 0)] * b
         ptrs = [t.data_ptr() for t in bufs[:b]]
         for _ in range(2):
-            r.render_batch_device(ptrs, 1024, 1024, cams, 128, 8, n, 0)
+            r.render_batch_device(ptrs, S, S, cams, a.steps, 8, n, 0)
         r.synchronize()
         t0 = time.perf_counter()
         for _ in range(max(1, a.frames // b)):
-            r.render_batch_device(ptrs, 1024, 1024, cams, 128, 8, n, 0)
+            r.render_batch_device(ptrs, S, S, cams, a.steps, 8, n, 0)
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
         line.append(f"batch {b}: {dt:.3f} ms/frame")
-    print(f"n={n} {a.schedule} bpc {a.bpc} rays {a.rays}: " + "  ".join(line), flush=True)
+    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays}: " + "  ".join(line), flush=True)

@@ -5,9 +5,13 @@ DESIGN.md / BASELINE.md.  Runs on the GPU box; prints one JSON object per config
   C4  plane_2 4096^2, bf16, 128 steps: the full frame on one GPU, and one rank's shard
       of the 8-way row-band split (what each GPU of the 8-GPU job renders)
   C5  each bundled geometry at 2048^2, fp16, 128 steps (one geometry per GPU)
-Per config: median frame time over --frames renders (HIP events around the launch on
-the context's stream, from nr_stats.ms_total), ray-steps, Mray-steps/s and the
-matrix-core fraction of the precision's dense peak."""
+Per config, two schedules:
+  single  median frame time over --frames renders, one nr_render launch per frame (HIP
+          events around the launch on the context's stream, from nr_stats.ms_total);
+  batch   --batch frames through one nr_render_batch launch (the bench's schedule: the
+          pixel queue runs through the frames, so one frame's longest rays overlap the
+          next frame's bulk), per-frame time = launch time / frames.
+Ray-steps, Mray-steps/s and the fraction of the precision's dense matrix peak."""
 import argparse
 import json
 import os
@@ -24,31 +28,47 @@ PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}
 FLOP = 14592
 ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=10)
+ap.add_argument("--batch", type=int, default=8, help="frames per nr_render_batch launch (0: skip)")
+ap.add_argument("--only", default="", help="comma-separated config names to run (default all)")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 
 
-def run(name, geom, size, prec, steps, shard=None):
-    r = nr.Renderer(0).load_h5(nr.geometry_path(geom)).set_precision(prec)
-    r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
-    rows = size if shard is None else nr.shard_rows(size, 8, 8, shard)
-    out = torch.zeros(rows * size, dtype=torch.int32, device="cuda")
-    ms = []
-    for i in range(a.frames + 2):
-        if shard is None:
-            st = r.render_device(out.data_ptr(), size, size, steps, with_stats=True)
-        else:
-            st = r.render_shard_device(out.data_ptr(), size, size, 8, 8, shard, steps, with_stats=True)
-        if i >= 2:
-            ms.append(st["ms_total"])
-    t = float(np.median(ms))
-    evals = st["ray_steps"] + st["shade_evals"]
+def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1):
+    evals = (st["ray_steps"] + st["shade_evals"]) / nframes
+    rs = st["ray_steps"] / nframes
     res = {"config": name, "geometry": geom, "size": size, "precision": prec, "max_steps": steps,
-           "shard": shard, "ms_per_frame": round(t, 4), "ray_steps": st["ray_steps"],
-           "Mray_steps_per_s": round(st["ray_steps"] / t / 1e3, 1),
+           "shard": shard, "schedule": sched, "ms_per_frame": round(t, 4), "ray_steps": int(rs),
+           "Mray_steps_per_s": round(rs / t / 1e3, 1),
            "TFLOPs": round(evals * FLOP / t / 1e9, 2),
            "frac_of_peak": round(evals * FLOP / t / 1e9 / PEAK[prec], 4)}
     print(json.dumps(res), flush=True)
+
+
+def run(name, geom, size, prec, steps, shard=None):
+    if a.only and name not in a.only.split(","):
+        return
+    r = nr.Renderer(0).load_h5(nr.geometry_path(geom)).set_precision(prec)
+    r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
+    band, nsh = (8, 8) if shard is not None else (8, 1)
+    rows = nr.shard_rows(size, band, nsh, shard or 0)
+    out = torch.zeros(max(a.batch, 1), rows * size, dtype=torch.int32, device="cuda")
+    ms = []
+    for i in range(a.frames + 2):
+        st = r.render_shard_device(out[0].data_ptr(), size, size, band, nsh, shard or 0, steps, with_stats=True)
+        if i >= 2:
+            ms.append(st["ms_total"])
+    report(name, geom, size, prec, steps, shard, "single", float(np.median(ms)), st)
+    if a.batch > 0:
+        iv, nm = nr.camera(0.0, 0.0, 2.0)
+        cams = [(iv, nm, 0)] * a.batch
+        ptrs = [out[i].data_ptr() for i in range(a.batch)]
+        ms = []
+        for i in range(4):
+            st = r.render_batch_device(ptrs, size, size, cams, steps, band, nsh, shard or 0, with_stats=True)
+            if i >= 1:
+                ms.append(st["ms_total"])
+        report(name, geom, size, prec, steps, shard, f"batch{a.batch}", float(np.median(ms)) / a.batch, st, a.batch)
     r.close()
 
 
