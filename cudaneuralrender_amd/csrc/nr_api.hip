@@ -164,7 +164,7 @@ int upload_lowp(nr_ctx *c) {
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
-    if (!pack_lowp_16(c->dims, c->kernels, c->biases, c->precision, a, f))
+    if (!pack_lowp_32(c->dims, c->kernels, c->biases, c->precision, a, f))
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
     return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
 }

@@ -42,17 +42,29 @@ constexpr int MAX_HIDDEN = 16;
 NR_HD constexpr inline int pk_final(int nh) { return PK_HID + nh * PK_HID_STRIDE; }
 NR_HD constexpr inline int pk_floats(int nh) { return pk_final(nh) + 36; }
 
-// Low-precision (bf16/fp16) hidden-layer A operands, 16-bit elements per layer:
-// [row tile 2][lane 64][8] for v_mfma_f32_16x16x32_{bf16,f16}; a separate float array
-// holds layer 0 (f32 MFMA), the hidden biases and the final layer.
-constexpr int LP_A_ELEMS = 2 * 64 * 8;
+// Low-precision (bf16/fp16) pack for the 32-point-tile MLP (nr_mlp16.h, mlp32_lowp):
+// v_mfma_f32_32x32x16_{bf16,f16}, lane l = (row / point r = l & 31, half h = l >> 5).
+// 16-bit elements (a_ops):
+//   [0, 512)                    layer-0 A operand [lane 64][8]: K = 16 slots holding the
+//                               hi/lo split of weights and inputs (w*x ~ wh*xh + wh*xl + wl*xh)
+//   LP32_HID + j*LP32_HSTRIDE   hidden layer j: A operand [k-step 2][lane 64][8]; element e of
+//                               lane half h in k-step s multiplies unit 16s + 8(e>>2) + 4h + (e&3)
+//                               (the accumulator-as-B-operand order of the previous layer)
+//   lp32_final(nh)              final layer: row 0 of the A operand only, [k-step 2][h 2][8]
+// floats (fl): biases as accumulator inits, [h 2][register 16] per layer (register i of half
+// h = unit (i&3) + 8(i>>2) + 4h): layer 0 at 0, hidden j at 32 + 32j, final bias at 32 + 32nh.
+constexpr int LP32_HID = 512;
+constexpr int LP32_HSTRIDE = 1024;
+NR_HD constexpr inline int lp32_final(int nh) { return LP32_HID + nh * LP32_HSTRIDE; }
+NR_HD constexpr inline int lp32_elems(int nh) { return lp32_final(nh) + 32; }
+NR_HD constexpr inline int lp32_floats(int nh) { return 32 + 32 * nh + 4; }
 
 bool fused_shape_ok(const std::vector<int> &dims);
 // Keras kernels (in x out, row-major) -> packs.  Return false if the shape is not
 // [3|4, 32, ..., 32, 1] (those networks render on the layered schedule).
 bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
-bool pack_lowp_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, int precision,
                   std::vector<uint16_t> &a_ops, std::vector<float> &bias);
 

@@ -1,5 +1,6 @@
-// nr_mlp16.h -- the MLP on 16-point MFMA tiles (v_mfma_f32_16x16x4_f32 for fp32,
-// v_mfma_f32_16x16x32_{bf16,f16} for reduced precision).
+// nr_mlp16.h -- the MLP on the matrix cores: 16-point tiles of v_mfma_f32_16x16x4_f32 for
+// fp32 (below), 32-point tiles of v_mfma_f32_32x32x16_{bf16,f16} for reduced precision
+// (mlp32_lowp_nt further down).
 //
 // A wave holds 64 points, point p in lane p.  They form 4 tiles of 16 points
 // (tile t = points 16t..16t+15); inside a tile lane (j, g) = (lane & 15, lane >> 4)
@@ -122,105 +123,159 @@ __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0
     return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
 }
 
-// bf16 / fp16 hidden layers: one v_mfma_f32_16x16x32 per row tile per layer (K = 32
-// in a single instruction, bias preloaded as the accumulator); layer 0 on the f32
-// matrix core as in the fp32 path; final layer in fp32 on VALU.  Register k = 4mt + r
-// of group g holds unit 16mt + 4g + r (the MFMA C layout, unpermuted).
-// bias + ReLU of one tile's two accumulators straight into the packed 16-bit B operand
-// of the next layer: v_cvt_pk_{bf16,f16}_f32 rounds pairs (RNE), v_pk_max_i16 against 0
-// is the ReLU on the 16-bit patterns (negative values and -0 have the sign bit set) --
-// 8 VALU per tile instead of 8 fmaxf + 4 conversions.
+// bf16 / fp16: the whole MLP on 32-point tiles, v_mfma_f32_32x32x16_{bf16,f16} (nr_internal.h
+// LP32_*).  The wave's 64 points form two tiles (points 0-31, 32-63); in a tile, lane l
+// feeds point l & 31 and the k-slots 8h..8h+7 of its half h = l >> 5.
+//   * layer 0 on the matrix core too: one K = 16 MFMA per tile over the hi/lo split of
+//     weights and inputs (w x ~ wh xh + wh xl + wl xh: ~2^-16 relative, f32 accumulate),
+//     bias as the accumulator init;
+//   * hidden layers: two K = 16 MFMAs per tile (K = 32), bias as the accumulator init; the
+//     f32 result is its own next B operand with no lane movement (registers 8s..8s+7 are
+//     k-step s, the pack orders the weights to match): per tile and layer 8
+//     v_cvt_pk + 8 v_pk_max_i16 (the ReLU on the 16-bit patterns) against 2 MFMAs of 32
+//     cycles -- the 16x16x32 form needed as many VALU per point for half the MFMA time
+//     per instruction and held the issue port twice as long per point;
+//   * final 32 -> 1 layer: two MFMAs with the weights in row 0 of A, z in register 0 of
+//     lanes 0-31; one v_permlane32_swap returns tile 1's z to lanes 32-63.
+// The lane-half views of the inputs come from v_permlane32_swap as well (no ds_bpermute).
+template <int PREC> struct Lowp;
+template <> struct Lowp<NR_PRECISION_BF16> { typedef __bf16 e; typedef bf16x8 v8; };
+template <> struct Lowp<NR_PRECISION_FP16> { typedef _Float16 e; typedef f16x8 v8; };
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// v0 = v of lane (l & 31), v1 = v of lane 32 + (l & 31)
+__device__ __forceinline__ void half_views(float v, float &v0, float &v1) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v0 = __uint_as_float(r[0]);
+    v1 = __uint_as_float(r[1]);
+}
+
 template <int PREC>
-__device__ __forceinline__ void relu_pack(const f32x4 &c0, const f32x4 &c1, uint32_t ap[4]) {
-    typedef typename std::conditional<PREC == NR_PRECISION_BF16, __bf16, _Float16>::type e16;
+__device__ __forceinline__ f32x16 mfma32(const typename Lowp<PREC>::v8 &a, const typename Lowp<PREC>::v8 &b,
+                                         const f32x16 &c) {
+    if constexpr (PREC == NR_PRECISION_BF16) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int PREC>
+__device__ __forceinline__ uint32_t pk16(typename Lowp<PREC>::e lo, typename Lowp<PREC>::e hi) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+}
+
+// registers 8s..8s+7 of an accumulator -> ReLU'd 16-bit B operand of k-step s:
+// v_cvt_pk rounds pairs (RNE), v_pk_max_i16 against 0 is the ReLU on the 16-bit patterns
+// (negative values and -0 have the sign bit set).  (The VOP3 clamp bit of v_cvt_pk would
+// fold the ReLU into the conversion for activations pre-scaled below 1 --
+// tools/cvt_clamp_probe.hip -- but the compiler inserts no MFMA->VALU wait states before
+// inline asm, and no builtin exposes the bit.)
+template <int PREC>
+__device__ __forceinline__ typename Lowp<PREC>::v8 relu_pack8(const f32x16 &c, int s) {
+    typedef typename Lowp<PREC>::e e16;
     typedef e16 e16x2 __attribute__((ext_vector_type(2)));
     typedef short s16x2 __attribute__((ext_vector_type(2)));
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const f32x2 v[4] = {{c0[0], c0[1]}, {c0[2], c0[3]}, {c1[0], c1[1]}, {c1[2], c1[3]}};
+    u32x4 w;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const s16x2 h = __builtin_bit_cast(s16x2, __builtin_convertvector(v[q], e16x2));
-        ap[q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (s16x2){0, 0}));
+        const f32x2 v = {c[8 * s + 2 * q], c[8 * s + 2 * q + 1]};
+        const s16x2 h = __builtin_bit_cast(s16x2, __builtin_convertvector(v, e16x2));
+        w[q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (s16x2){0, 0}));
     }
+    return __builtin_bit_cast(typename Lowp<PREC>::v8, w);
 }
 
-template <int PREC>
-__device__ __forceinline__ f32x4 mfma_lowp(const void *w, const uint32_t ap[4], const f32x4 &cinit) {
-    typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const v8 b = __builtin_bit_cast(v8, (u32x4){ap[0], ap[1], ap[2], ap[3]});
-    if constexpr (PREC == NR_PRECISION_BF16)
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const v8 *>(w), b, cinit, 0, 0, 0);
-    else
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(*reinterpret_cast<const v8 *>(w), b, cinit, 0, 0, 0);
+__device__ __forceinline__ f32x16 load_bias16(const float *b) {
+    const float4 *q = reinterpret_cast<const float4 *>(b);
+    const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+    return f32x16{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
 }
 
+// one hidden layer on NT tiles: acc <- W relu(acc) + b
 template <int PREC, int NT>
-__device__ __forceinline__ float mlp16_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                               int nh, float fr, float x, float y, float z) {
-    typedef typename std::conditional<PREC == NR_PRECISION_BF16, bf16x8, f16x8>::type v8;
-    const int lane = lane_id(), g = lane >> 4, j = lane & 15;
-    uint32_t ap[NT][4];  // activations of the hidden layers, packed 16-bit B operands
-    float a[NT][8];      // fp32 activations feeding the final layer
-    f32x4 c0[NT], c1[NT];
-    {
-        const float w0 = fl[lane], w1 = fl[64 + lane];
-        const float4 *bb = reinterpret_cast<const float4 *>(fl + 128 + g * 8);
-        const float4 blo = bb[0], bhi = bb[1];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
-            const float pw = in0 == 4 ? __shfl(fr, 16 * t + j) : 0.0f;
-            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : pw));
-            c0[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{blo.x, blo.y, blo.z, blo.w}, 0, 0, 0);
-            c1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{bhi.x, bhi.y, bhi.z, bhi.w}, 0, 0, 0);
-        }
-    }
-    // hidden layers; the last one's output stays fp32 for the final layer
-    // (tile t's pack is issued right before its MFMAs, so it overlaps tile t-1's)
-    for (int jl = 0; jl < nh; ++jl) {
-        const v8 *A = reinterpret_cast<const v8 *>(lp + (size_t)jl * LP_A_ELEMS);
-        const v8 w0 = A[lane], w1 = A[64 + lane];
-        const float4 *bb = reinterpret_cast<const float4 *>(fl + 160 + 32 * jl + g * 8);
-        const float4 blo = bb[0], bhi = bb[1];
-        const f32x4 c0i = {blo.x, blo.y, blo.z, blo.w}, c1i = {bhi.x, bhi.y, bhi.z, bhi.w};
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            relu_pack<PREC>(c0[t], c1[t], ap[t]);
-            c0[t] = mfma_lowp<PREC>(&w0, ap[t], c0i);
-            c1[t] = mfma_lowp<PREC>(&w1, ap[t], c1i);
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            a[t][r] = fmaxf(c0[t][r], 0.0f);
-            a[t][4 + r] = fmaxf(c1[t][r], 0.0f);
-        }
-    const float *wf = fl + 160 + 32 * nh + g * 8;
-    const float bf = fl[160 + 32 * nh + 32];
-    float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+__device__ __forceinline__ void hidden32(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int jl,
+                                         f32x16 (&acc)[NT]) {
+    typedef typename Lowp<PREC>::v8 v8;
+    const int lane = lane_id(), h = lane >> 5;
+    const v8 *A = reinterpret_cast<const v8 *>(lp + LP32_HID + jl * LP32_HSTRIDE);
+    const v8 a0 = A[lane], a1 = A[64 + lane];
+    const f32x16 bj = load_bias16(fl + 32 + 32 * jl + 16 * h);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(wf[k], a[t][k], acc);
-        acc += __shfl_xor(acc, 16);
-        acc += __shfl_xor(acc, 32);
-        zt[t] = acc + bf;
+        const v8 k0 = relu_pack8<PREC>(acc[t], 0), k1 = relu_pack8<PREC>(acc[t], 1);
+        acc[t] = mfma32<PREC>(a1, k1, mfma32<PREC>(a0, k0, bj));
     }
-    return tile_outputs(zt);
 }
 
+template <int PREC, int NT, int NH>
+__device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                               int nh_rt, float fr, float x, float y, float z) {
+    typedef typename Lowp<PREC>::e e16;
+    typedef typename Lowp<PREC>::v8 v8;
+    const int nh = NH > 0 ? NH : nh_rt;
+    const int lane = lane_id(), h = lane >> 5;
+    const uint32_t hm = 0u - (uint32_t)h;  // all ones in the upper half
+    f32x16 acc[NT];
+    {
+        float xv[2], yv[2], zv[2], fv[2];
+        half_views(x, xv[0], xv[1]);
+        half_views(y, yv[0], yv[1]);
+        half_views(z, zv[0], zv[1]);
+        if (in0 == 4) half_views(fr, fv[0], fv[1]);
+        else fv[0] = fv[1] = 0.0f;
+        const v8 A = reinterpret_cast<const v8 *>(lp)[lane];
+        const f32x16 b0 = load_bias16(fl + 16 * h);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const e16 xh = (e16)xv[t], yh = (e16)yv[t], zh = (e16)zv[t], fh = (e16)fv[t];
+            const e16 xl = (e16)(xv[t] - (float)xh), yl = (e16)(yv[t] - (float)yh);
+            const e16 zl = (e16)(zv[t] - (float)zh), flo = (e16)(fv[t] - (float)fh);
+            // h = 0: {xh, yh, zh, xl, yl, zl, fh, fl}; h = 1: {xh, yh, zh, fh, 0, 0, 0, 0}
+            // (bit selects, so that nothing is computed under a lane-dependent branch)
+            const uint32_t w0 = pk16<PREC>(xh, yh);
+            const uint32_t w1 = (pk16<PREC>(zh, xl) & ~hm) | (pk16<PREC>(zh, fh) & hm);
+            const uint32_t w2 = pk16<PREC>(yl, zl) & ~hm;
+            const uint32_t w3 = pk16<PREC>(fh, flo) & ~hm;
+            acc[t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){w0, w1, w2, w3}), b0);
+        }
+    }
+    if constexpr (NH > 0) {
+#pragma unroll
+        for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT>(lp, fl, jl, acc);
+    } else {
+        for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT>(lp, fl, jl, acc);
+    }
+    // final layer: row 0 of A (lanes 0 and 32) holds the weights, every other row is 0;
+    // the accumulator starts at 0 and the bias is added to register 0 alone
+    const uint16_t *F = lp + lp32_final(nh);
+    v8 f0 = {}, f1 = {};
+    if ((lane & 31) == 0) {
+        f0 = reinterpret_cast<const v8 *>(F)[h];
+        f1 = reinterpret_cast<const v8 *>(F)[2 + h];
+    }
+    const float bf = fl[32 + 32 * nh];
+    float zt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const v8 k0 = relu_pack8<PREC>(acc[t], 0), k1 = relu_pack8<PREC>(acc[t], 1);
+        zt[t] = mfma32<PREC>(f1, k1, mfma32<PREC>(f0, k0, f32x16{}))[0] + bf;
+    }
+    if constexpr (NT == 1) return zt[0];
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
+    return __uint_as_float(r[0]);
+}
+
+// tmask: the caller's 16-point tiles (bits 0-3); the 32-point tiles cover pairs of them
 template <int PREC>
 __device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                             int nh, float fr, float x, float y, float z, uint32_t tmask) {
-    const int nt = 32 - __clz((int)tmask);
-    if (nt >= 4) return mlp16_lowp_nt<PREC, 4>(lp, fl, in0, nh, fr, x, y, z);
-    if (nt == 3) return mlp16_lowp_nt<PREC, 3>(lp, fl, in0, nh, fr, x, y, z);
-    if (nt == 2) return mlp16_lowp_nt<PREC, 2>(lp, fl, in0, nh, fr, x, y, z);
-    return mlp16_lowp_nt<PREC, 1>(lp, fl, in0, nh, fr, x, y, z);
+    // the bundled networks' depth (7 hidden layers) fully unrolled: no loop-carried
+    // accumulator copies between layers
+    if (nh == 7) {
+        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7>(lp, fl, in0, nh, fr, x, y, z);
+        return mlp32_lowp_nt<PREC, 1, 7>(lp, fl, in0, nh, fr, x, y, z);
+    }
+    if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 0>(lp, fl, in0, nh, fr, x, y, z);
+    return mlp32_lowp_nt<PREC, 1, 0>(lp, fl, in0, nh, fr, x, y, z);
 }
 
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,

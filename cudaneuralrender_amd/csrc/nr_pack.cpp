@@ -45,6 +45,20 @@ uint16_t f2fp16(float x) {
     if (exp >= 31) return (uint16_t)(sign | 0x7c00u);
     return (uint16_t)(sign | (uint32_t)exp << 10 | (uint32_t)mant);
 }
+
+float bf16f(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f; memcpy(&f, &u, 4);
+    return f;
+}
+
+float fp16f(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const float sign = (h & 0x8000u) ? -1.0f : 1.0f;
+    if (e == 31) return m ? NAN : sign * INFINITY;
+    if (e == 0) return sign * std::ldexp((float)m, -24);
+    return sign * std::ldexp((float)(1024 + m), e - 25);
+}
 }  // namespace
 
 // ---- 16-point tiles (nr_mlp16.h).  Lane (j, g): point j, unit group g; register k.
@@ -52,8 +66,6 @@ namespace {
 // fp32: unit held by (g, k): next layer MFMA -> 4k + g (ascending f32 chain over the
 // 8 k-steps x 4 lane groups); next layer final VALU -> 8g + k (chain hops 3 times).
 inline int unit16(int g, int k, bool final_consumer) { return final_consumer ? 8 * g + k : 4 * k + g; }
-// low precision: the MFMA C layout as is: register k = 4mt + r of group g = row 16mt + 4g + r
-inline int row16(int g, int k) { return 16 * (k >> 2) + 4 * g + (k & 3); }
 }  // namespace
 
 bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
@@ -95,39 +107,54 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
     return true;
 }
 
-bool pack_lowp_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
                   const std::vector<std::vector<float>> &B, int precision, std::vector<uint16_t> &a_ops,
                   std::vector<float> &fl) {
     if (!fused_shape_ok(dims)) return false;
-    int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
-    auto cvt = [&](float v) { return precision == NR_PRECISION_BF16 ? f2bf16(v) : f2fp16(v); };
-    a_ops.assign((size_t)nh * LP_A_ELEMS, 0);
-    fl.assign(160 + 32 * nh + 36, 0.0f);
-    // layer 0: f32 16x16x4 MFMA A operand, rows in natural unit order
-    for (int mt = 0; mt < 2; ++mt)
-        for (int lane = 0; lane < 64; ++lane) {
-            int i = lane & 15, kk = lane >> 4;
-            fl[mt * 64 + lane] = (kk < in0) ? K[0][(size_t)kk * 32 + 16 * mt + i] : 0.0f;
+    const int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    const bool bf = precision == NR_PRECISION_BF16;
+    auto cvt = [&](float v) { return bf ? f2bf16(v) : f2fp16(v); };
+    auto back = [&](uint16_t h) { return bf ? bf16f(h) : fp16f(h); };
+    auto lo = [&](float v) { return cvt(v - back(cvt(v))); };  // the residual's 16-bit value
+    auto crow = [](int h, int i) { return (i & 3) + 8 * (i >> 2) + 4 * h; };      // C/D row of register i
+    auto kin = [](int s, int h, int e) { return 16 * s + 8 * (e >> 2) + 4 * h + (e & 3); };
+    a_ops.assign((size_t)lp32_elems(nh), 0);
+    fl.assign((size_t)lp32_floats(nh), 0.0f);
+    // layer 0, K = 16: h = 0 slots {wh x3 . xh, wh x3 . xl, wh3 . frh, wh3 . frl},
+    //                  h = 1 slots {wl x3 . xh, wl3 . frh, 0 x4}
+    for (int lane = 0; lane < 64; ++lane) {
+        const int m = lane & 31, h = lane >> 5;
+        uint16_t *e = &a_ops[(size_t)lane * 8];
+        for (int c = 0; c < 3; ++c) {
+            const float w = K[0][(size_t)c * 32 + m];
+            if (h == 0) e[c] = e[3 + c] = cvt(w);
+            else e[c] = lo(w);
         }
-    for (int g = 0; g < 4; ++g)
-        for (int k = 0; k < 8; ++k) fl[128 + g * 8 + k] = B[0][row16(g, k)];
+        if (in0 == 4) {
+            const float w = K[0][(size_t)3 * 32 + m];
+            if (h == 0) e[6] = e[7] = cvt(w);
+            else e[3] = lo(w);
+        }
+    }
+    for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 16; ++i) fl[h * 16 + i] = B[0][crow(h, i)];
     for (int j = 0; j < nh; ++j) {
         const std::vector<float> &Kj = K[j + 1];
-        for (int mt = 0; mt < 2; ++mt)
+        for (int s = 0; s < 2; ++s)
             for (int lane = 0; lane < 64; ++lane)
                 for (int e = 0; e < 8; ++e) {
-                    int i = lane & 15, gg = lane >> 4;
-                    int uin = row16(gg, e);       // B operand element e of group gg = that unit
-                    int uout = 16 * mt + i;
-                    a_ops[(size_t)j * LP_A_ELEMS + (mt * 64 + lane) * 8 + e] = cvt(Kj[(size_t)uin * 32 + uout]);
+                    const int m = lane & 31, h = lane >> 5;
+                    a_ops[(size_t)LP32_HID + (size_t)j * LP32_HSTRIDE + (size_t)s * 512 + lane * 8 + e] =
+                        cvt(Kj[(size_t)kin(s, h, e) * 32 + m]);
                 }
-        for (int g = 0; g < 4; ++g)
-            for (int k = 0; k < 8; ++k) fl[160 + 32 * j + g * 8 + k] = B[j + 1][row16(g, k)];
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) fl[32 + 32 * j + h * 16 + i] = B[j + 1][crow(h, i)];
     }
-    int fo = 160 + 32 * nh;
-    for (int g = 0; g < 4; ++g)
-        for (int k = 0; k < 8; ++k) fl[fo + g * 8 + k] = K[nl - 1][row16(g, k)];
-    fl[fo + 32] = B[nl - 1][0];
+    for (int s = 0; s < 2; ++s)
+        for (int h = 0; h < 2; ++h)
+            for (int e = 0; e < 8; ++e)
+                a_ops[(size_t)lp32_final(nh) + (s * 2 + h) * 8 + e] = cvt(K[nl - 1][kin(s, h, e)]);
+    fl[32 + 32 * nh] = B[nl - 1][0];
     return true;
 }
 

@@ -322,26 +322,34 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
 }
 
 // Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
-// 16-point-tile path: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks.
+// matrix-core tiles: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks; the next
+// chunk's inputs are loaded before the current chunk's MLP, so their HBM latency (~2 us)
+// hides behind its MFMAs instead of stalling every wave once per chunk.
 template <int PREC>
 __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
     Smem16 S = stage16(M, PREC);
     const int lane = lane_id();
     const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-    for (long base = wave * 64; base < n; base += nwaves * 64) {
-        const long i = base + lane;
-        const bool live = i < n;
-        float x = 0.0f, y = 0.0f, z = 0.0f, f = 0.0f;
-        if (live) {
+    const long stride = (((long)gridDim.x * blockDim.x) >> 6) * 64;
+    auto load = [&](long i, float &x, float &y, float &z, float &f) {
+        x = y = z = f = 0.0f;
+        if (i < n) {
             const float *p = X + i * M.in0;
             x = p[0]; y = p[1]; z = p[2];
             if (M.in0 == 4) f = p[3];
         }
+    };
+    long base = wave * 64;
+    float nx, ny, nz, nf;
+    load(base + lane, nx, ny, nz, nf);
+    for (; base < n; base += stride) {
+        const long i = base + lane;
+        const float x = nx, y = ny, z = nz, f = nf;
+        load(base + stride + lane, nx, ny, nz, nf);
         const long rem = n - base;
         const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
         const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask);
-        if (live) Y[i] = v;
+        if (i < n) Y[i] = v;
     }
 }
 
