@@ -26,6 +26,29 @@ namespace nr {
 #define NR_TRACE_BPC 3
 #endif
 
+// Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
+// issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
+// (issue arbitration is priority, then age), so it is back in its MLP sooner and the
+// matrix pipe idles less: fp32 batch 2.050 -> 2.012 ms/frame (prio 1/2/3: 2.018/2.016/
+// 2.012; profiles/r1_ab_experiments.txt).  0 = off.  fp32 only (bf16: +1%).
+#ifndef NR_NONMLP_PRIO
+#define NR_NONMLP_PRIO 3
+#endif
+
+// Wave-private pools of pixel-queue positions reserved one atomic ahead (bf16/fp16
+// tracers only: their iterations are short, so the ~1 us reservation latency is a large
+// part of the refill; the fp32 tracer's MLP hides it and the pools only lengthen the
+// tail -- tools/ab_multi.sh, profiles/r1_ab_experiments.txt).
+#ifndef NR_QUEUE_PREFETCH_LOWP
+#define NR_QUEUE_PREFETCH_LOWP 1
+#endif
+#ifndef NR_QUEUE_CHUNK
+#define NR_QUEUE_CHUNK 32
+#endif
+#ifndef NR_QUEUE_LOW
+#define NR_QUEUE_LOW 8
+#endif
+
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
 
@@ -76,6 +99,8 @@ __device__ __forceinline__ void set_priority(int prio) {
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
 __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
+    constexpr bool QPF = NR_QUEUE_PREFETCH_LOWP && PREC != NR_PRECISION_FP32;  // queue pools
+    constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
         const int nw = T.nframes * (int)(sizeof(FrameArgs) / 4);
@@ -99,6 +124,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     const int nq = 1 << T.nq_shift;  // pixel-queue shards
     int shard = blockIdx.x & (nq - 1), tries = 0;
     bool qempty = false;
+    uint32_t pool_base = 0, pool_cnt = 0, pend_v = 0;  // NR_QUEUE_PREFETCH state
+    bool pend = false;
     bool hold = false;  // age hold (TraceArgs::hold_age): no refill, packed tiles, raised priority
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
     float tfar = 0.0f;
@@ -122,9 +149,57 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             if (freem) {
                 const uint32_t nfree = (uint32_t)__popcll(freem);
                 uint32_t base = 0, got = 0;
+                auto shard_total = [&](int sh) -> long {
+                    const long sh_chunks = sh < nchunks ? ((nchunks - 1 - sh) >> T.nq_shift) + 1 : 0;
+                    return (PROBE ? sh_chunks : sh_chunks * 64) * (BATCH ? T.nframes : 1);
+                };
+                if constexpr (QPF) {
+                // Positions come from a wave-private pool of reserved queue positions; the
+                // next reservation is requested (one atomic, not waited for) when the pool
+                // runs low and absorbed when it is empty, so its ~1 us return latency
+                // overlaps the MLP instead of stalling the refill.
+                if (pool_cnt == 0) {
+                    if (pend) {
+                        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend_v);
+                        pend = false;
+                        const long tot = shard_total(shard);
+                        if ((long)b < tot) {
+                            pool_base = b;
+                            pool_cnt = (uint32_t)min((long)NR_QUEUE_CHUNK, tot - (long)b);
+                        }
+                    }
+                    while (pool_cnt == 0) {  // nothing reserved: a blocking reservation
+                        const long tot = shard_total(shard);
+                        const uint32_t want = max(nfree, (uint32_t)NR_QUEUE_CHUNK);
+                        uint32_t b = 0;
+                        if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, want);
+                        b = (uint32_t)__shfl((int)b, 0);
+                        if ((long)b < tot) {
+                            pool_base = b;
+                            pool_cnt = (uint32_t)min((long)want, tot - (long)b);
+                            break;
+                        }
+                        shard = (shard + 1) & (nq - 1);
+                        if (++tries >= nq) {
+                            qempty = true;
+                            if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
+                            break;
+                        }
+                    }
+                }
+                if (pool_cnt) {
+                    base = pool_base;
+                    got = min(nfree, pool_cnt);
+                    pool_base += got;
+                    pool_cnt -= got;
+                }
+                if (!qempty && !pend && pool_cnt < NR_QUEUE_LOW) {
+                    if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)NR_QUEUE_CHUNK);
+                    pend = true;
+                }
+                } else {
                 while (true) {
-                    const long sh_chunks = shard < nchunks ? ((nchunks - 1 - shard) >> T.nq_shift) + 1 : 0;
-                    const long total = (PROBE ? sh_chunks : sh_chunks * 64) * (BATCH ? T.nframes : 1);
+                    const long total = shard_total(shard);
                     uint32_t b = 0;
                     if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
                     base = __shfl(b, 0);
@@ -138,6 +213,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                         if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
                         break;
                     }
+                }
                 }
                 if (got) {
                     const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
@@ -241,7 +317,9 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             }
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
+        if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask);
+        if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
