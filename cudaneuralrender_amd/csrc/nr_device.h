@@ -115,16 +115,14 @@ __device__ __forceinline__ float smooth_union(float d1, float d2, float k) {  //
     // Reference: h = __saturatef(0.5 + 0.5*(d2-d1)/k); mix = d2*(1.0-h) + d1*h;
     // return mix - k*h*(1.0-h), with the double literals promoting to f64.
     // When |d2-d1| >= k the f64 quotient is >= 0.5 in magnitude (division and rounding
-    // are monotone, 0.5 is representable), so h is exactly 1 or 0; every remaining
-    // product is then by 0 or 1 and every sum adds a zero, all exact in f32, so the f32
-    // evaluation below is bit-identical to the f64 one (signed zeros included).
+    // are monotone, 0.5 is representable), so h is exactly 1 or 0, and what remains is
+    // exact in f32: h = 1 gives (d2*0 + d1) - (+0) = d2*0 + d1, h = 0 gives
+    // (d2 + d1*0) - (+0) = d1*0 + d2 -- each one fmaf, since the product by 0 is exact
+    // (signed zeros and NaN/inf operands included; proven on the CPU against the reference
+    // form, tests/test_oracle.py).
     const float t = d2 - d1;
-    if (t >= k || t <= -k) {
-        const float h = (t >= k) ? 1.0f : 0.0f;
-        const float omh = 1.0f - h;
-        const float mix = d2 * omh + d1 * h;
-        return mix - (k * h) * omh;
-    }
+    if (t >= k) return __builtin_fmaf(d2, 0.0f, d1);
+    if (t <= -k) return __builtin_fmaf(d1, 0.0f, d2);
     const float h = saturatef_((float)(0.5 + 0.5 * (double)t / (double)k));
     const float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
     return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
@@ -149,23 +147,20 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     const float xx[3] = {x0 * x0, x1 * x1, x2 * x2};
     const float yy[3] = {y0 * y0, y1 * y1, y2 * y2};
     const float zz = zc * zc;
-    float s = nsdf;
+    // All 9 sphere distances first -- 9 independent correctly rounded square roots the
+    // wave issues back to back -- then the sequential smooth-union chain, which is the
+    // reference's loop in the reference's order (length(cP) = sqrtf(dot(cP, cP))).  In a
+    // wave of scattered rays nearly every sphere has some lane near it, so skipping the
+    // square roots of far spheres behind a branch cost more than it saved
+    // (tools/scene_bench.hip).
+    float d[9];
 #pragma unroll
     for (int row = 0; row < 3; ++row)
 #pragma unroll
-        for (int col = 0; col < 3; ++col) {
-            // Far sphere: if |cP| > s + 0.1111 with s + 0.1111 < 1000, d2 = |cP| - 0.1
-            // exceeds s by more than k = 0.01 plus every rounding error of |cP|, d2 and
-            // d2 - s (each < 1e-4 at these magnitudes), so smooth_union takes h = 1 and
-            // returns (d2 * 0 + s) - 0 = s + 0 (d2 > 0 whenever s is a zero; finite sq
-            // keeps d2 * 0 from being NaN) -- decided without the correctly rounded sqrt.
-            const float sq = (xx[col] + yy[row]) + zz;
-            const float T = s + 0.1111f;
-            if (T > 0.0f && T < 1000.0f && sq > T * T && sq < 1e30f)
-                s = s + 0.0f;
-            else
-                s = smooth_union(s, sqrtf(sq) - 0.1f, 0.01f);  // length(cP) = sqrtf(dot(cP, cP))
-        }
+        for (int col = 0; col < 3; ++col) d[3 * row + col] = sqrtf((xx[col] + yy[row]) + zz) - 0.1f;
+    float s = nsdf;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s = smooth_union(s, d[i], 0.01f);
     return s;
 }
 

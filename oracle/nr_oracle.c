@@ -511,12 +511,8 @@ float or_smooth_union_ref(float d1, float d2, float k) { return sdfOpSmoothUnion
 float or_smooth_union_kernelform(float d1, float d2, float k)
 {
     const float t = d2 - d1;
-    if (t >= k || t <= -k) {
-        const float h = (t >= k) ? 1.0f : 0.0f;
-        const float omh = 1.0f - h;
-        const float mix = d2 * omh + d1 * h;
-        return mix - (k * h) * omh;
-    }
+    if (t >= k) return fmaf(d2, 0.0f, d1);    /* h = 1: d2*0 + d1 */
+    if (t <= -k) return fmaf(d1, 0.0f, d2);   /* h = 0: d1*0 + d2 */
     const float h = saturatef((float)(0.5 + 0.5 * (double)t / (double)k));
     const float mix = (float)((double)d2 * (1.0 - (double)h) + (double)(d1 * h));
     return (float)((double)mix - (double)(k * h) * (1.0 - (double)h));
@@ -535,17 +531,11 @@ float or_many_sphere_kernelform(float px, float py, float pz, float nsdf, int fr
     const float xx[3] = { x0 * x0, x1 * x1, x2 * x2 };
     const float yy[3] = { y0 * y0, y1 * y1, y2 * y2 };
     const float zz = zc * zc;
-    float s = nsdf;
+    float d[9];
     for (int row = 0; row < 3; ++row)
-        for (int col = 0; col < 3; ++col)
-        {
-            const float sq = (xx[col] + yy[row]) + zz;
-            const float T = s + 0.1111f;
-            if (T > 0.0f && T < 1000.0f && sq > T * T && sq < 1e30f)   /* sphere farther than s + k: the union returns s */
-                s = s + 0.0f;
-            else
-                s = or_smooth_union_kernelform(s, sqrtf(sq) - 0.1f, 0.01f);
-        }
+        for (int col = 0; col < 3; ++col) d[3 * row + col] = sqrtf((xx[col] + yy[row]) + zz) - 0.1f;
+    float s = nsdf;
+    for (int i = 0; i < 9; ++i) s = or_smooth_union_kernelform(s, d[i], 0.01f);
     return s;
 }
 

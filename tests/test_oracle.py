@@ -107,8 +107,15 @@ def test_smooth_union_kernel_form_bit_exact():
     edge = np.concatenate([d1[:1000] + k, d1[:1000] - k, np.nextafter(d1[:1000] + k, 0), np.zeros(4)]).astype(np.float32)
     d1 = np.concatenate([d1, d1[:1000], d1[:1000], d1[:1000], [0.0, -0.0, 0.0, -0.0]]).astype(np.float32)
     d2 = np.concatenate([d2, edge[:3000], [0.0, 0.0, -0.0, -0.0]]).astype(np.float32)
+    # signed zeros, infinities, NaN and huge values on either side (the fmaf forms of the
+    # saturated cases must keep the reference's signs and NaN/inf behaviour)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e38, -1e38, 1e-45, -1e-45, 0.01, -0.01], np.float32)
+    a, b = np.meshgrid(sp, sp)
+    d1 = np.concatenate([d1, a.ravel()]).astype(np.float32)
+    d2 = np.concatenate([d2, b.ravel()]).astype(np.float32)
     ref, ker = oracle.smooth_union_pair(d1, d2, 0.01)
-    assert np.array_equal(ref.view(np.uint32), ker.view(np.uint32))
+    same = (ref.view(np.uint32) == ker.view(np.uint32)) | (np.isnan(ref) & np.isnan(ker))
+    assert same.all(), (d1[~same][:5], d2[~same][:5], ref[~same][:5], ker[~same][:5])
 
 
 @pytest.mark.parametrize("frame", [0, 7, 359])
