@@ -49,6 +49,17 @@ namespace nr {
 #define NR_QUEUE_LOW 8
 #endif
 
+// Refill only once this many ray slots are free (or the wave is empty), so that the ray
+// generation and the queue bookkeeping are paid for several rays at a time: bf16 batch
+// 0.611 -> 0.571 ms/frame at 8 (4: 0.589, 16: 0.575), fp32 1.978 -> 1.964 at 4
+// (profiles/r1_ab_experiments.txt).
+#ifndef NR_REFILL_MIN_LOWP
+#define NR_REFILL_MIN_LOWP 8
+#endif
+#ifndef NR_REFILL_MIN_FP32
+#define NR_REFILL_MIN_FP32 4
+#endif
+
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
 
@@ -101,6 +112,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     constexpr int prec = PREC;
     constexpr bool QPF = NR_QUEUE_PREFETCH_LOWP && PREC != NR_PRECISION_FP32;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
+    constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
         const int nw = T.nframes * (int)(sizeof(FrameArgs) / 4);
@@ -146,8 +158,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
             const uint64_t freem = __ballot(!live) & T.lane_cap;
-            if (freem) {
-                const uint32_t nfree = (uint32_t)__popcll(freem);
+            const uint32_t nfree = (uint32_t)__popcll(freem);
+            if (nfree >= (uint32_t)RMIN || (nfree && nfree == (uint32_t)T.take)) {
                 uint32_t base = 0, got = 0;
                 auto shard_total = [&](int sh) -> long {
                     const long sh_chunks = sh < nchunks ? ((nchunks - 1 - sh) >> T.nq_shift) + 1 : 0;
