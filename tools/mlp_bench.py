@@ -44,6 +44,6 @@ for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else [a.precision]
         ms = e0.elapsed_time(e1) / a.iters
         tf = a.n * 14592 / (ms * 1e-3) / 1e12
         util = a.n * 14336 / (ms * 1e-3) / 1e12 / PEAK[prec]
-        res.append({"precision": prec, "tile": "16", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
+        res.append({"precision": prec, "tile": "16" if prec == "fp32" else "32", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
                     "hidden_layer_mfma_util": round(util, 4), "Gpoints_per_s": round(a.n / ms / 1e6, 2)})
         print(json.dumps(res[-1]), flush=True)
