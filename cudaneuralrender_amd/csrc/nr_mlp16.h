@@ -89,6 +89,42 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
     }
     if constexpr (PART != 0) return a[0][0] + a[NT - 1][7];
+    if constexpr (NT >= 3) {
+        // final 32 -> 1 for 3-4 tiles: a 4x4 transpose of (tile, lane group) blocks with
+        // v_permlane32_swap + v_permlane16_swap puts all 32 units of point j of tile t in
+        // lane (j, t) -- the point's own lane -- so one 32-long fmaf chain (units ascending,
+        // the oracle's order) serves all four tiles at once: 32 swaps + 33 VALU against
+        // 4 x 38 for per-tile chains handed across groups (every VALU instruction costs
+        // f32 matrix time on gfx950, tools/mfma_peak.hip)
+        float b[4][8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            uint32_t t0 = __float_as_uint(a[0][k]), t1 = __float_as_uint(a[1][k]);
+            uint32_t t2 = __float_as_uint(a[2][k]), t3 = NT > 3 ? __float_as_uint(a[NT > 3 ? 3 : 0][k]) : 0u;
+            auto r = __builtin_amdgcn_permlane32_swap(t0, t2, false, false);  // groups 2,3 <-> 0,1
+            t0 = r[0]; t2 = r[1];
+            r = __builtin_amdgcn_permlane32_swap(t1, t3, false, false);
+            t1 = r[0]; t3 = r[1];
+            r = __builtin_amdgcn_permlane16_swap(t0, t1, false, false);       // groups 1,3 <-> 0,2
+            t0 = r[0]; t1 = r[1];
+            r = __builtin_amdgcn_permlane16_swap(t2, t3, false, false);
+            t2 = r[0]; t3 = r[1];
+            b[0][k] = __uint_as_float(t0); b[1][k] = __uint_as_float(t1);
+            b[2][k] = __uint_as_float(t2); b[3][k] = __uint_as_float(t3);
+        }
+        const float4 *wf4 = reinterpret_cast<const float4 *>(s + pk_final(nh));
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const float4 w = wf4[q];  // units 4q..4q+3 = group q >> 1, registers 4(q & 1)..+3
+            const int gg = q >> 1, k0 = 4 * (q & 1);
+            acc = __builtin_fmaf(w.x, b[gg][k0 + 0], acc);
+            acc = __builtin_fmaf(w.y, b[gg][k0 + 1], acc);
+            acc = __builtin_fmaf(w.z, b[gg][k0 + 2], acc);
+            acc = __builtin_fmaf(w.w, b[gg][k0 + 3], acc);
+        }
+        return acc + s[pk_final(nh) + 32];
+    }
     // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
     // groups 0 -> 1 -> 2 -> 3 with one cross-lane hand-off per group.
     const float *wf = s + pk_final(nh) + g * 8;
