@@ -52,7 +52,7 @@ struct nr_ctx {
     int temporal = 0;
     // age hold (nr_set_age_hold)
     int hold_age = 0, hold_prio = 2;
-    int spread = 16;  // nr_set_pixel_spread (16: measured 2-3% faster than block-major on configs[1])
+    int spread = -1;  // nr_set_pixel_spread; -1 = auto (spread_for)
     int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
     int wave_rays = 64;  // nr_set_wave_rays
     int nq_shift = 3;    // nr_set_queue_shards: 8
@@ -118,6 +118,21 @@ int set_err(nr_ctx *c, int code, const char *fmt, ...) {
     if (c) c->err = buf;
     g_err = buf;
     return code;
+}
+
+// Pixel spread of a launch of `nframes` frames of `npix` pixels each (nr_set_pixel_spread;
+// -1 = auto).  One frame deals groups of 16 blocks pixel-major, so one slow block's rays
+// spread over many waves and the frame's tail is shorter (fp32 2.649 -> 2.517 ms).  A batch
+// hides the tails behind the next frame's bulk, and block-major dealing (coherent waves: one
+// 8x8 block per refill) is faster there: bf16 at every batch size (1024^2 x 32: 0.568 ->
+// 0.519 ms/frame, one 8-way shard: 0.087 -> 0.081), fp32 once a launch holds >= 8 M pixels
+// (1024^2 x 32: 1.961 -> 1.908; one 8-way shard x 32 frames, 4 M: 0.290 vs 0.293).
+// Measurements: profiles/r1_ab_experiments.txt.
+int spread_for(const nr_ctx *c, int nframes, size_t npix) {
+    if (c->spread >= 0) return c->spread;
+    if (nframes < 4) return 16;
+    if (c->precision != NR_PRECISION_FP32) return 0;
+    return (size_t)nframes * npix >= ((size_t)8 << 20) ? 0 : 16;
 }
 
 #define HIPCHK(ctx, expr)                                                                            \
@@ -800,7 +815,10 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
     T.hold_prio = c->hold_prio & 3;
     T.hold_refill = c->hold_prio >= 4;
-    T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
+    {
+        const int sp = spread_for(c, nframes, npix);
+        T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;
+    }
     T.inv_bw = 1.0 / (double)T.bw;
     T.inv_band = 1.0 / (double)band;
     T.take = c->wave_rays;
@@ -914,7 +932,10 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.hold_prio = c->hold_prio & 3;
         T.hold_refill = c->hold_prio >= 4;
         T.itmap = (c->debug & 8) != 0;
-        T.spread_shift = c->spread > 1 ? 31 - __builtin_clz((unsigned)c->spread) : 0;
+        {
+            const int sp = spread_for(c, 1, npix);
+            T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;
+        }
         T.inv_bw = 1.0 / (double)T.bw;
         T.inv_band = 1.0 / (double)band;
         T.take = c->wave_rays;
@@ -1164,8 +1185,9 @@ int nr_set_age_hold(nr_ctx *c, int age, int prio) {
 }
 
 int nr_set_pixel_spread(nr_ctx *c, int group_blocks) {
-    if (!c || group_blocks < 0 || group_blocks > 65536 || (group_blocks & (group_blocks - 1)))
-        return set_err(c, NR_E_INVALID, "nr_set_pixel_spread: group_blocks must be 0 or a power of two <= 65536");
+    if (!c || group_blocks < -1 || group_blocks > 65536 || (group_blocks > 0 && (group_blocks & (group_blocks - 1))))
+        return set_err(c, NR_E_INVALID,
+                       "nr_set_pixel_spread: group_blocks must be -1 (auto), 0 or a power of two <= 65536");
     c->spread = group_blocks;
     return NR_OK;
 }

@@ -25,6 +25,10 @@ namespace nr {
 #ifndef NR_TRACE_BPC
 #define NR_TRACE_BPC 3
 #endif
+// diagnostic build: every pixel write is an atomicAdd of 1 << 24 (tools/lowp_wcount.py)
+#ifndef NR_DBG_WCOUNT
+#define NR_DBG_WCOUNT 0
+#endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
@@ -41,6 +45,9 @@ namespace nr {
 // tail -- tools/ab_multi.sh, profiles/r1_ab_experiments.txt).
 #ifndef NR_QUEUE_PREFETCH_LOWP
 #define NR_QUEUE_PREFETCH_LOWP 1
+#endif
+#ifndef NR_QUEUE_PREFETCH_FP32
+#define NR_QUEUE_PREFETCH_FP32 0
 #endif
 #ifndef NR_QUEUE_CHUNK
 #define NR_QUEUE_CHUNK 32
@@ -110,7 +117,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
 __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
-    constexpr bool QPF = NR_QUEUE_PREFETCH_LOWP && PREC != NR_PRECISION_FP32;  // queue pools
+    constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
@@ -130,6 +137,13 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     auto out_of = [&](int f) -> uint32_t * { return BATCH ? sf[f].out : A.out; };
     auto zoff_of = [&](int f) -> double { return BATCH ? sf[f].zoff : zoff0; };
     auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
+    auto put = [&](int f, uint32_t i, uint32_t v) {
+#if NR_DBG_WCOUNT
+        atomicAdd(out_of(f) + i, 0x01000000u | (v & 0xffffffu));
+#else
+        out_of(f)[i] = v;
+#endif
+    };
     const int q4 = lane & 3;
     const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
     int nstash = 0;
@@ -143,8 +157,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     float tfar = 0.0f;
     uint32_t pix = 0;
     int rf = 0;  // the ray's frame (BATCH)
-    int it = 0, maxit = 0;
-    bool live = false;
+    int it = -1, maxit = 0;  // it: iterations of the slot's ray; -1: no ray (an int, not a
+                             // bool, so that the compiler keeps it in a VGPR, not a lane mask)
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
     unsigned long long ph[5] = {0, 0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene, step
@@ -153,11 +167,20 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
     while (true) {
         if constexpr (timing) tph = __builtin_amdgcn_s_memtime();
+        // The loop's control state is wave-uniform (the whole wave is active here);
+        // readfirstlane lets the compiler keep it in SGPRs and branch on it as such.
+        nstash = __builtin_amdgcn_readfirstlane(nstash);
+        qempty = __builtin_amdgcn_readfirstlane((int)qempty) != 0;
+        shard = __builtin_amdgcn_readfirstlane(shard);
+        tries = __builtin_amdgcn_readfirstlane(tries);
+        pool_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_base);
+        pool_cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_cnt);
+        pend = __builtin_amdgcn_readfirstlane((int)pend) != 0;
         // ---- refill free slots from the pixel queue
         if (!qempty && !(hold && !T.hold_refill)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
-            const uint64_t freem = __ballot(!live) & T.lane_cap;
+            const uint64_t freem = __ballot(it < 0) & T.lane_cap;
             const uint32_t nfree = (uint32_t)__popcll(freem);
             if (nfree >= (uint32_t)RMIN || (nfree && nfree == (uint32_t)T.take)) {
                 uint32_t base = 0, got = 0;
@@ -165,6 +188,9 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                     const long sh_chunks = sh < nchunks ? ((nchunks - 1 - sh) >> T.nq_shift) + 1 : 0;
                     return (PROBE ? sh_chunks : sh_chunks * 64) * (BATCH ? T.nframes : 1);
                 };
+                // Queue positions are broadcast with readfirstlane (the whole wave is active
+                // here), not __shfl, so that the compiler sees them as uniform and keeps the
+                // queue logic in scalar branches instead of lane-mask control flow.
                 if constexpr (QPF) {
                 // Positions come from a wave-private pool of reserved queue positions; the
                 // next reservation is requested (one atomic, not waited for) when the pool
@@ -185,7 +211,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                         const uint32_t want = max(nfree, (uint32_t)NR_QUEUE_CHUNK);
                         uint32_t b = 0;
                         if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, want);
-                        b = (uint32_t)__shfl((int)b, 0);
+                        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);  // lane 0: the whole wave is active
                         if ((long)b < tot) {
                             pool_base = b;
                             pool_cnt = (uint32_t)min((long)want, tot - (long)b);
@@ -214,7 +240,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                     const long total = shard_total(shard);
                     uint32_t b = 0;
                     if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
-                    base = __shfl(b, 0);
+                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
                     if ((long)base < total) {
                         got = (uint32_t)min((long)nfree, total - (long)base);
                         break;
@@ -230,7 +256,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                 if (got) {
                     const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
                     bool hit = false;
-                    if (!live && rank < got) {
+                    if (it < 0 && rank < got) {
                         uint32_t q = base + rank;
                         int f = 0;
                         if constexpr (BATCH) {  // frame-major: frame f owns [f * per, (f + 1) * per)
@@ -263,12 +289,11 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                         if (px < A.W && py < A.rows) {
                             hit = gen_ray(A, T, BATCH ? sf[f].inv_view : A.inv_view, px, py, p, d, tfar);
                             if (hit && A.max_steps > 0) {
-                                live = true;
                                 it = 0;
                                 pix = (uint32_t)lp;
                                 rf = f;
                             } else if (!PROBE) {
-                                out_of(f)[lp] = 0u;  // background (:335-339) or no iterations at all
+                                put(f, lp, 0u);  // background (:335-339) or no iterations at all
                             }
                         }
                     }
@@ -281,7 +306,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
         // its size, and the marching rays must not wait for it.
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
-        uint64_t lm = __ballot(live);
+        uint64_t lm = __ballot(it >= 0);
         while (nstash >= 16 || (qempty && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
             const int k = lane >> 2;
@@ -299,8 +324,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
             if (k < nb && q4 == 0 && !T.itmap) {
                 const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                out_of(sfr)[__float_as_uint(sp.w)] =
-                    shade_color(A, BATCH ? sf[sfr].normal : A.normal, nrm, mk3(sd.x, sd.y, sd.z));
+                put(sfr, __float_as_uint(sp.w),
+                    shade_color(A, BATCH ? sf[sfr].normal : A.normal, nrm, mk3(sd.x, sd.y, sd.z)));
             }
             nconv += (uint64_t)nb;
             nstash -= nb;
@@ -322,9 +347,9 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                 tfar = __shfl(tfar, src);
                 pix = (uint32_t)__shfl((int)pix, src);
                 if constexpr (BATCH) rf = __shfl(rf, src);
-                it = __shfl(it, src);
-                live = lane < nl;
-                lm = __ballot(live);
+                const int it_src = __shfl(it, src);
+                it = lane < nl ? it_src : -1;
+                lm = __ballot(it >= 0);
                 tmask = (1u << need) - 1u;
             }
         }
@@ -341,7 +366,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         ++wit;
         wit_tail += qempty ? 1u : 0u;
         bool conv = false;
-        if (live) {
+        if (it >= 0) {
             const float ts = scene_sdf(p, sdf, A.scene, zoff_of(rf));
             if constexpr (timing) {
                 __builtin_amdgcn_s_waitcnt(0);
@@ -351,29 +376,27 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
             if (tfar <= 0) {
-                if (!PROBE) out_of(rf)[pix] = 0u;
-                live = false;
+                if (!PROBE) put(rf, pix, 0u);
                 used = it + 1;
             } else {
                 p = add3(p, mul3s(d, ts));
                 if (ts < MARCHING_EPSILON) {
-                    live = false;
                     if (it + 1 < A.max_steps) {  // coloured in the next iteration (:446-457)
                         conv = !PROBE;
                         used = it + 2;
                     } else {
-                        if (!PROBE) out_of(rf)[pix] = 0u;
+                        if (!PROBE) put(rf, pix, 0u);
                         used = it + 1;
                     }
                 } else if (++it >= A.max_steps) {  // iteration cap: pixel stays 0 (:690)
-                    if (!PROBE) out_of(rf)[pix] = 0u;
-                    live = false;
+                    if (!PROBE) put(rf, pix, 0u);
                     used = A.max_steps;
                 }
             }
-            if (used) {
+            if (used) {  // the ray ended
+                it = -1;
                 maxit = max(maxit, used);
-                if (!PROBE && T.itmap) out_of(rf)[pix] = (uint32_t)used;
+                if (!PROBE && T.itmap) put(rf, pix, (uint32_t)used);
                 if (T.bcost) {
                     const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
                     atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
@@ -388,7 +411,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         }
         nstash += (int)__popcll(cm);
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; tph = t; }
-        const bool h = __ballot(live && it >= T.hold_age) != 0;
+        const bool h = __ballot(it >= 0 && it >= T.hold_age) != 0;
         if (h != hold) {
             hold = h;
             set_priority(h ? T.hold_prio : 0);

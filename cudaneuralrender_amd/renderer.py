@@ -205,7 +205,8 @@ class Renderer:
 
     def set_pixel_spread(self, group_blocks):
         """Persistent schedule: deal each group of `group_blocks` 8x8 blocks pixel-major
-        (default 16; 0 = block-major)."""
+        (0 = block-major; -1 = automatic, the default: 16 for one-frame launches, 0 for
+        nr_render_batch launches of 4 or more frames)."""
         self._chk(self._L.nr_set_pixel_spread(self._ctx, int(group_blocks)))
         return self
 
