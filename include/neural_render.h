@@ -216,8 +216,9 @@ int nr_set_age_hold(nr_ctx *ctx, int age, int prio);
 /* Pixel spread (persistent schedule): the pixel queue deals each group of
  * `group_blocks` 8x8 blocks pixel-major -- one refill takes one pixel from each of up
  * to 64 blocks -- so the rays of one slow block are spread over many waves (0 =
- * block-major; -1 = automatic, the default: 16 for launches of fewer than 4 frames, 0 for
- * larger nr_render_batch launches).  Pixels are unaffected. */
+ * block-major; -1 = automatic, the default: 16 for launches of fewer than 4 frames and
+ * for fp32 batches of under 8 M pixels in all, 0 for the other nr_render_batch launches).
+ * Pixels are unaffected. */
 int nr_set_pixel_spread(nr_ctx *ctx, int group_blocks);
 /* Cost probe (persistent schedule): before each frame, march the centre ray of every
  * 8x8 block for at most `max_steps` iterations (`rays_per_wave` rays per wave, so the
