@@ -4,7 +4,7 @@
 set -e
 run() {
   timeout -k 10 120 python tools/batch_bench.py --frames 64 --batches 1,32 --shards 1,8
-  timeout -k 10 120 python tools/batch_bench.py --frames 64 --batches 1,32 --shards 1,8 --precision bf16
+  [ -n "$FP32_ONLY" ] || timeout -k 10 120 python tools/batch_bench.py --frames 64 --batches 1,32 --shards 1,8 --precision bf16
 }
 echo "== default"; run
 for alt in "$@"; do echo "== $alt"; NR_LIBRARY=$PWD/$alt/libnr.so run; done

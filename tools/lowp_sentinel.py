@@ -1,7 +1,7 @@
 """Diagnostic: repeated batched renders into device images pre-filled with a sentinel; counts
 pixels never written and pixels that differ from the single-frame render, and repeats the
 single-frame renders (GPU box).
-    python tools/lowp_sentinel.py PREC TRIALS [BATCH_OCCUPANCY [SINGLE_OCCUPANCY]]
+    python tools/lowp_sentinel.py PREC TRIALS [BATCH_OCCUPANCY [SINGLE_OCCUPANCY [FRAMES [WxH]]]]
 (occupancy: workgroups per CU of the persistent grid, nr_set_occupancy; 0 = automatic)."""
 import os
 import sys
@@ -16,12 +16,13 @@ prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
 trials = int(sys.argv[2]) if len(sys.argv) > 2 else 12
 occ_b = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 occ_s = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+ncams = int(sys.argv[5]) if len(sys.argv) > 5 else 6
+W, H = (int(v) for v in sys.argv[6].split("x")) if len(sys.argv) > 6 else (160, 144)
 dims, K, B = nr.read_keras_h5(nr.geometry_path("car_1"))
 r = nr.Renderer(0).load_mlp(dims, K, B).set_precision(prec).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
 r.set_matcap(nr.load_png(nr.matcap_path("Chrome")))
-W, H = 160, 144
 rng = np.random.default_rng(11)
-cams = [(*nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0), 0) for _ in range(6)]
+cams = [(*nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0), 0) for _ in range(ncams)]
 ref, tot = [], np.zeros(3, np.int64)
 for iv, nm, fr in cams:
     r.set_view(iv, nm, fr)
