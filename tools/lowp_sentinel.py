@@ -19,7 +19,7 @@ occ_s = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 ncams = int(sys.argv[5]) if len(sys.argv) > 5 else 6
 W, H = (int(v) for v in sys.argv[6].split("x")) if len(sys.argv) > 6 else (160, 144)
 dims, K, B = nr.read_keras_h5(nr.geometry_path("car_1"))
-r = nr.Renderer(0).load_mlp(dims, K, B).set_precision(prec).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
+r = nr.Renderer(0).load_mlp(dims, K, B).set_precision(prec).set_static(int(os.environ.get("NR_COLOR", nr.NR_COLOR_MATCAP)), 3).set_scene("v1")
 r.set_matcap(nr.load_png(nr.matcap_path("Chrome")))
 rng = np.random.default_rng(11)
 cams = [(*nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0), 0) for _ in range(ncams)]
