@@ -25,7 +25,8 @@ namespace nr {
 #ifndef NR_TRACE_BPC
 #define NR_TRACE_BPC 3
 #endif
-// diagnostic build: every pixel write is an atomicAdd of 1 << 24 (tools/lowp_wcount.py)
+// diagnostic builds: 1 = every pixel write is an atomicAdd of 1 << 24 (tools/lowp_wcount.py);
+// 2 = each pixel's top byte is 1 + the lane that marched its ray (tools/lowp_lanes.py)
 #ifndef NR_DBG_WCOUNT
 #define NR_DBG_WCOUNT 0
 #endif
@@ -138,8 +139,10 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     auto zoff_of = [&](int f) -> double { return BATCH ? sf[f].zoff : zoff0; };
     auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
     auto put = [&](int f, uint32_t i, uint32_t v) {
-#if NR_DBG_WCOUNT
+#if NR_DBG_WCOUNT == 1
         atomicAdd(out_of(f) + i, 0x01000000u | (v & 0xffffffu));
+#elif NR_DBG_WCOUNT == 2  // lane tag: the top byte is 1 + the lane that marched the ray
+        out_of(f)[i & 0xffffffu] = ((i >> 24 ? i >> 24 : (uint32_t)lane_id() + 1u) << 24) | (v & 0xffffffu);
 #else
         out_of(f)[i] = v;
 #endif
@@ -406,7 +409,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         const uint64_t cm = __ballot(conv);
         if (conv) {
             const int slot = nstash + (int)__popcll(cm & lanemask_lt());
-            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
+            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(NR_DBG_WCOUNT == 2 ? pix | ((uint32_t)lane + 1u) << 24 : pix));
             stash[wid][slot][1] = make_float4(d.x, d.y, d.z, __int_as_float(rf));
         }
         nstash += (int)__popcll(cm);
