@@ -25,11 +25,6 @@ namespace nr {
 #ifndef NR_TRACE_BPC
 #define NR_TRACE_BPC 3
 #endif
-// diagnostic builds: 1 = every pixel write is an atomicAdd of 1 << 24 (tools/lowp_wcount.py);
-// 2 = each pixel's top byte is 1 + the lane that marched its ray (tools/lowp_lanes.py)
-#ifndef NR_DBG_WCOUNT
-#define NR_DBG_WCOUNT 0
-#endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
@@ -67,6 +62,8 @@ namespace nr {
 #ifndef NR_REFILL_MIN_FP32
 #define NR_REFILL_MIN_FP32 4
 #endif
+
+typedef __attribute__((address_space(1))) uint32_t *gptr_u32;
 
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
@@ -135,18 +132,13 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     const float fr = (float)A.frame;
     const double zoff0 = sphere_zoff(A.frame);
     // frame-dependent values of frame f (single-frame launches: the uniform ones in A)
-    auto out_of = [&](int f) -> uint32_t * { return BATCH ? sf[f].out : A.out; };
+    // the output image of frame f as a global-address-space pointer: a batched frame's
+    // pointer comes from the LDS FrameArgs, and as a generic pointer its stores would be
+    // flat_store (counted on both vmcnt and lgkmcnt) instead of global_store
+    auto out_of = [&](int f) -> gptr_u32 { return (gptr_u32)(BATCH ? sf[f].out : A.out); };
     auto zoff_of = [&](int f) -> double { return BATCH ? sf[f].zoff : zoff0; };
     auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
-    auto put = [&](int f, uint32_t i, uint32_t v) {
-#if NR_DBG_WCOUNT == 1
-        atomicAdd(out_of(f) + i, 0x01000000u | (v & 0xffffffu));
-#elif NR_DBG_WCOUNT == 2  // lane tag: the top byte is 1 + the lane that marched the ray
-        out_of(f)[i & 0xffffffu] = ((i >> 24 ? i >> 24 : (uint32_t)lane_id() + 1u) << 24) | (v & 0xffffffu);
-#else
-        out_of(f)[i] = v;
-#endif
-    };
+    auto put = [&](int f, uint32_t i, uint32_t v) { out_of(f)[i] = v; };
     const int q4 = lane & 3;
     const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
     int nstash = 0;
@@ -409,7 +401,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         const uint64_t cm = __ballot(conv);
         if (conv) {
             const int slot = nstash + (int)__popcll(cm & lanemask_lt());
-            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(NR_DBG_WCOUNT == 2 ? pix | ((uint32_t)lane + 1u) << 24 : pix));
+            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
             stash[wid][slot][1] = make_float4(d.x, d.y, d.z, __int_as_float(rf));
         }
         nstash += (int)__popcll(cm);
