@@ -13,7 +13,10 @@ longest rays march while the next frame's pixels keep the matrix cores busy -- e
 frame is rendered in full, none is reused.  config.single_frame repeats the timing with
 one nr_render call per frame (each launch waits for the previous frame's last ray).
 
-N > 1 runs under torch.distributed.run, one rank per GPU: rows are dealt round-robin one
+N > 1 runs one rank per GPU under torch.distributed.run: the driver's launcher, or, when
+`python bench.py --gpus N` is started without one (WORLD_SIZE unset), bench.py starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` itself as a child process
+before anything touches a GPU and exits with its status.  Rows are dealt round-robin one
 row at a time (band 1, nr_render_batch's shard arguments: the slowest of 8 ranks is within
 1% of the mean, against 6% for 8-row bands -- tools/shard_balance.py), each rank renders its rows of every
 frame, then one RCCL gather (torch.distributed.gather over the "nccl" backend) brings
@@ -21,13 +24,22 @@ the batch's shards to rank 0 -- one collective for the K frames, single-frame ti
 one per frame -- which re-interleaves each frame (nr_assemble_shards).  The frame size
 is fixed as N grows: scaling "strong".
 
+`value` = the ray-steps the timed launches themselves counted (nr_render_batch's stats,
+summed over ranks) / the max-over-ranks wall time of the timed region.  Every timed frame
+is checked against a reference render afterwards (config.parity_frames_checked).
+config.random_poses repeats the timing over 8 poses from default_rng(1) (rx in [-30, 30],
+ry in [0, 360), zoom 2), the K frames cycling through them.
+
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
-k_trace, f32 MFMA bound, per-launch HIP events on the stream it runs on) and
-`cpu_baseline` (the C oracle on the host cores, N = 1 only).
+k_trace, f32 MFMA bound, per-launch HIP events on the stream it runs on; per rank for
+N > 1) and `cpu_baseline` (the C oracle on the host cores, N = 1 only: all-core value
+plus a single-thread figure and the CPU model).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -58,21 +70,34 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(size, max_steps, threads, geometry, matcap, iv, nm):
-    """C oracle (oracle/nr_oracle.c, OpenMP over rays) on the host cores.
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
-    Sample: one full frame of the benchmark workload when it fits the 10-30 s budget,
-    else a 512^2 frame of the same camera/steps."""
+
+def cpu_baseline(size, max_steps, threads, geometry, matcap, iv, nm):
+    """C oracle (oracle/nr_oracle.c, OpenMP over rays) on the host cores, all-core and
+    single-thread.
+
+    All-core sample: one full frame of the benchmark workload when it fits ~30 s, else a
+    512^2 frame of the same camera/steps; single-thread sample: a 256^2 frame of the same
+    camera/steps (about 0.98 M ray-steps, a few seconds)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     import cudaneuralrender_amd as nr
     dims, K, B = nr.read_keras_h5(nr.geometry_path(geometry))
     net = oracle.OracleNet(K, B)
-    # calibrate on a 256^2 frame, then pick the sample
+    # single thread on 256^2 (also the calibration for the all-core sample)
     t0 = time.perf_counter()
-    _, st = net.render(256, 256, iv, nm, color_type=1, matcap=matcap, max_steps=max_steps, nthreads=threads)
-    rate = st["ray_steps"] / (time.perf_counter() - t0)
-    est_full = 15e6 * (size / 1024) ** 2 / max(rate, 1.0)
+    _, st1 = net.render(256, 256, iv, nm, color_type=1, matcap=matcap, max_steps=max_steps, nthreads=1)
+    dt1 = time.perf_counter() - t0
+    rate1 = st1["ray_steps"] / dt1
+    est_full = 15e6 * (size / 1024) ** 2 / max(rate1 * threads * 0.7, 1.0)
     s = size if est_full <= 30.0 else 512
     t0 = time.perf_counter()
     _, st = net.render(s, s, iv, nm, color_type=1, matcap=matcap, max_steps=max_steps, nthreads=threads)
@@ -80,12 +105,40 @@ def cpu_baseline(size, max_steps, threads, geometry, matcap, iv, nm):
     return {"value": round(st["ray_steps"] / dt / 1e6, 4), "unit": "Mray-steps/s", "cores": threads,
             "kind": "port",
             "sample": f"{geometry} {s}x{s}, {max_steps} steps, Chrome matcap, default camera: "
-                      f"{st['ray_steps']} ray-steps in {dt:.2f} s (C oracle, OpenMP, {threads} threads, "
-                      f"host {os.cpu_count()} logical CPUs)"}
+                      f"{st['ray_steps']} ray-steps in {dt:.2f} s (C oracle, OpenMP, {threads} threads)",
+            "single_thread": {"value": round(rate1 / 1e6, 4), "unit": "Mray-steps/s", "cores": 1,
+                              "sample": f"{geometry} 256x256, {max_steps} steps: {st1['ray_steps']} ray-steps "
+                                        f"in {dt1:.2f} s"},
+            "cpu_model": cpu_model(),
+            "host_logical_cpus": os.cpu_count(),
+            "threads_note": "the GPU box's CPU share is 16 threads (OMP_NUM_THREADS); os.cpu_count() "
+                            "reports the whole machine"}
+
+
+def random_poses(n=8):
+    """8 poses from default_rng(1), rx in U[-30, 30], ry in U[0, 360), zoom 2."""
+    rng = np.random.default_rng(1)
+    return [(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360))) for _ in range(n)]
+
+
+def self_launch(a):
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run, one
+    rank per GPU, as a child process (nothing here has touched a GPU), and return its status."""
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(self_launch(a))
     import torch
     import torch.distributed as dist
     import cudaneuralrender_amd as nr
@@ -130,32 +183,41 @@ def main():
                 r.assemble_device(gather.data_ptr() + i * shard_px * 4, nbuf * shard_px, frames[i0 + i].data_ptr(),
                                   size, size, BAND, world)
 
-    def run_batched(n):
+    default_cams = [(iv, nm, 0)]
+    pose_cams = [(*nr.camera(rx, ry, 2.0), 0) for rx, ry in random_poses()]
+    counted = {"ray_steps": 0, "shade_evals": 0}
+
+    def run_batched(n, cams=default_cams):
+        """n frames (cycling through cams) in one nr_render_batch call; the call's own
+        counters (read back at its end) are what `value` is computed from."""
         if n == 0:
             return
         with torch.cuda.stream(stream):
-            r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size, [(iv, nm, 0)] * n,
-                                  a.max_steps, BAND, world, rank)
+            st = r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size,
+                                       [cams[i % len(cams)] for i in range(n)], a.max_steps, BAND, world, rank,
+                                       with_stats=True)
+            counted["ray_steps"] += st["ray_steps"]
+            counted["shade_evals"] += st["shade_evals"]
             collect(0, n)
 
     def run_single(n):
         with torch.cuda.stream(stream):
             for i in range(n):
-                r.render_shard_device(shards[i].data_ptr(), size, size, BAND, world, rank, a.max_steps)
+                st = r.render_shard_device(shards[i].data_ptr(), size, size, BAND, world, rank, a.max_steps,
+                                           with_stats=True)
+                counted["ray_steps"] += st["ray_steps"]
+                counted["shade_evals"] += st["shade_evals"]
                 collect(i, 1)
 
-    # work per frame (deterministic): ray-steps of this rank's shard, summed over ranks
-    st = r.render_shard(size, size, BAND, world, rank, a.max_steps)[1]
-    steps_t = torch.tensor([st["ray_steps"], st["shade_evals"]], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(steps_t)
-    ray_steps, shade_evals = (float(v) for v in steps_t.tolist())
-
     def timed(fn, profile):
+        """W untimed warmup frames, then exactly K frames between barrier + synchronize;
+        returns (max-over-ranks seconds, this rank's k_trace profile, ray-steps and shade
+        evals the K frames counted, summed over ranks, and per-rank ray-steps)."""
         fn(a.warmup)
         torch.cuda.synchronize()
         r.prof_collect()          # drop anything recorded so far
         r.set_profiling(profile)
+        counted["ray_steps"] = counted["shade_evals"] = 0
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -167,53 +229,84 @@ def main():
         dt = time.perf_counter() - t0
         r.set_profiling(False)
         prof = r.prof_collect()
-        dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        mine = torch.tensor([dt, counted["ray_steps"], counted["shade_evals"]], dtype=torch.float64, device="cuda")
+        per_rank = [mine.clone() for _ in range(world)]
         if world > 1:
-            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-        return float(dt_t.item()), prof
+            dist.all_gather(per_rank, mine)
+        per_rank = torch.stack(per_rank).cpu().numpy()
+        return (float(per_rank[:, 0].max()), prof, float(per_rank[:, 1].sum()), float(per_rank[:, 2].sum()),
+                per_rank)
 
-    dt, prof = timed(run_batched, True)
-    last = frames[a.steps - 1] if frames is not None else None
-
-    # parity spot-check of the last timed frame (outside the timed region)
-    parity = None
-    if rank == 0:
-        ref = r.render(size, size, a.max_steps, with_stats=False)
+    def check_frames(n, cams):
+        """Every timed frame against a full single-GPU nr_render of its camera (rank 0, after
+        the timed region): returns (all equal, frames checked)."""
+        if rank != 0:
+            return None, 0
+        refs = {}
+        ok = True
+        for i in range(n):
+            k = i % len(cams)
+            if k not in refs:
+                r.set_view(cams[k][0], cams[k][1], 0)
+                img = r.render(size, size, a.max_steps, with_stats=False)
+                refs[k] = torch.from_numpy(img.view(np.int32).reshape(-1)).to("cuda")
+            got = frames[i][: size * size]
+            ok = ok and bool(torch.equal(got, refs[k]))
+        r.set_view(iv, nm, 0)
         torch.cuda.synchronize()
-        got = last.cpu().numpy().view(np.uint32)[: size * size].reshape(size, size)
-        parity = bool(np.array_equal(ref, got))
+        return ok, n
+
+    dt, prof, ray_steps_k, shade_evals_k, per_rank = timed(run_batched, True)
+    rank_steps = per_rank[:, 1]
+    parity, nchecked = check_frames(a.steps, default_cams)
 
     dt_single = None
     if not a.no_single_frame:
-        dt_single, _ = timed(run_single, False)
+        dt_single, _, rs_single, _, _ = timed(run_single, False)
+
+    # the same timing over 8 random poses (SURVEY.md §8(d)), frames cycling through them
+    dt_pose, _, rs_pose, se_pose, _ = timed(lambda n: run_batched(n, pose_cams), False)
+    pose_parity, pose_checked = check_frames(a.steps, pose_cams)
 
     # roofline of the dominant kernel (k_trace) from this rank's per-launch events
     launches = max(prof["march_launches"], 1)
     march_avg_ms = prof["march_ms"] / launches
     # k_trace evaluates the MLP for every march step AND the 4 tetrahedral samples of
-    # every coloured ray (in-kernel shading), 14,592 algorithmic FLOP each
-    local_evals = (st["ray_steps"] + st["shade_evals"]) * prof["renders"]
+    # every coloured ray (in-kernel shading), 14,592 algorithmic FLOP each; this rank's
+    # evals are its own counted ray-steps + shade evals of the timed frames
+    local_evals = float(per_rank[rank, 1] + per_rank[rank, 2])
     flop_per_launch = local_evals * FLOP_PER_EVAL / launches
     achieved = flop_per_launch / (march_avg_ms * 1e-3) / 1e12 if march_avg_ms > 0 else 0.0
     peak = PEAK[a.precision]
+    roof_t = torch.tensor([achieved, march_avg_ms], dtype=torch.float64, device="cuda")
+    roof_all = [roof_t.clone() for _ in range(world)]
+    if world > 1:
+        dist.all_gather(roof_all, roof_t)
+    roof_all = torch.stack(roof_all).cpu().numpy()
 
     # HBM traffic of k_trace from the PMC pass committed under profiles/ (rocprofv3 --pmc
-    # FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 2x fetch correction) when it was
-    # collected on this workload; bench.py cannot read PMC counters itself
-    traffic = None
-    try:
-        tp = json.load(open(os.path.join(REPO, "profiles", "r1_pmc_traffic.json")))
-        if (a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1
-                and tp.get("frames_per_launch") == min(a.steps, MAX_BATCH)):
-            traffic = tp["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        traffic = None
+    # FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 corrections), per frame of this
+    # workload, times the frames of one launch; bench.py cannot read PMC counters itself
+    traffic, traffic_src = None, None
+    for name in ("r2_pmc_traffic.json", "r1_pmc_traffic.json"):
+        try:
+            tp = json.load(open(os.path.join(REPO, "profiles", name)))
+        except (OSError, ValueError):
+            continue
+        if a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1:
+            per_frame = tp.get("hbm_bytes_per_frame")
+            if per_frame is None and tp.get("frames_per_launch"):
+                per_frame = tp["hbm_bytes_per_launch"] / tp["frames_per_launch"]
+            if per_frame:
+                traffic = int(per_frame * min(a.steps, MAX_BATCH))
+                traffic_src = name
+        break
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
-    value = ray_steps * a.steps / dt / 1e6
+    value = ray_steps_k / dt / 1e6
     out = {
         "metric": "Mray-steps/s at 1024^2, plane_1.h5 (frames/s in config.fps)",
         "value": round(value, 3),
@@ -231,19 +324,33 @@ def main():
             "workload": f"{a.geometry} {size}x{size}, {a.max_steps} march steps, {a.precision}, Chrome.png, "
                         "v1 scene, default camera (BASELINE configs[1])",
             "fps": round(a.steps / dt, 3),
-            "ray_steps_per_frame": int(ray_steps),
-            "shade_evals_per_frame": int(shade_evals),
+            "ray_steps_counted": int(ray_steps_k),
+            "ray_steps_per_frame": int(ray_steps_k / a.steps),
+            "shade_evals_per_frame": int(shade_evals_k / a.steps),
             "frames_per_launch": min(a.steps, MAX_BATCH),
             "schedule": "nr_render_batch: the K timed frames through one frame-major pixel queue "
                         "(every frame rendered in full)",
-            "parallelism": f"row-band shards x{world} + one RCCL gather per batch of frames" if world > 1
-                           else "single GPU",
+            "parallelism": f"row-band shards x{world} (band {BAND}) + one RCCL gather per batch of frames"
+                           if world > 1 else "single GPU",
             "parity_vs_single_gpu_render": parity,
+            "parity_frames_checked": nchecked,
+            "shard_ray_steps": {"max": int(rank_steps.max()), "mean": round(float(rank_steps.mean()), 1)}
+                               if world > 1 else None,
             "single_frame": None if dt_single is None else {
-                "value": round(ray_steps * a.steps / dt_single / 1e6, 3),
+                "value": round(rs_single / dt_single / 1e6, 3),
                 "ms_per_step": round(dt_single / a.steps * 1e3, 4),
                 "fps": round(a.steps / dt_single, 3),
                 "schedule": "one nr_render_shard launch per frame",
+            },
+            "random_poses": {
+                "value": round(rs_pose / dt_pose / 1e6, 3),
+                "ms_per_step": round(dt_pose / a.steps * 1e3, 4),
+                "fps": round(a.steps / dt_pose, 3),
+                "ray_steps_per_frame": int(rs_pose / a.steps),
+                "shade_evals_per_frame": int(se_pose / a.steps),
+                "poses": "8 from default_rng(1): rx U[-30,30], ry U[0,360), zoom 2; frames cycle through them",
+                "parity_vs_single_gpu_render": pose_parity,
+                "parity_frames_checked": pose_checked,
             },
         },
         "roofline": {
@@ -254,12 +361,14 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per launch (profiles/r1_pmc_traffic.json)",
+            "traffic_unit": f"HBM bytes per launch (per-frame PMC figure x frames per launch, profiles/{traffic_src})"
+                            if traffic is not None else None,
             "flop_per_launch": round(flop_per_launch, 1),
             "avg_launch_ms": round(march_avg_ms, 5),
             "launches": int(prof["march_launches"]),
-            "flop_basis": "(ray-steps + shade evals) x 14,592 FLOP per frame x frames per launch / mean k_trace "
-                          "launch duration (per-launch HIP events on the context stream)",
+            "flop_basis": "(ray-steps + shade evals the launch counted) x 14,592 FLOP / mean k_trace launch "
+                          "duration (per-launch HIP events on the context stream), rank 0",
+            "per_rank_frac": [round(float(x) / peak, 4) for x in roof_all[:, 0]] if world > 1 else None,
         },
         "cpu_baseline": None,
     }

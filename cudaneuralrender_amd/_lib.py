@@ -26,7 +26,7 @@ EXPORTS = [
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
-    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk",
+    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
 ]
 
 
@@ -109,6 +109,7 @@ def lib():
         "nr_render_shard": (I, [P, P, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_shard_rows": (I, [I, I, I, I]),
+        "nr_batch_frames_per_launch": (I, [I, I, I, I, I, I, I]),
         "nr_assemble_shards": (I, [P, P, ctypes.c_size_t, P, I, I, I, I, I]),
         "nr_mlp_forward": (I, [P, P, P, L64, I]),
         "nr_layer_forward": (I, [P, I, P, P, L64, I]),

@@ -796,7 +796,9 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (npix == 0) { if (stats) *stats = st; return NR_OK; }
     GET_STREAM(c, s);
     int rc;
-    const int chunk = std::min(nframes, NR_MAX_BATCH);
+    const int chunk = nr_batch_frames_per_launch(W, H, band, nshards, shard, nframes, 1 << c->nq_shift);
+    if (chunk < 1)
+        return set_err(c, NR_E_INVALID, "nr_render_batch: %dx%d shard overflows the 32-bit pixel queue", W, H);
     if ((rc = upload_frames(c, frames, nframes, npix, loc, chunk, s)) != NR_OK) return rc;
 
     RenderArgs A{};
@@ -868,6 +870,21 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         HIPCHK(c, hipStreamSynchronize(s));
     }
     return NR_OK;
+}
+
+// Queue positions are uint32 (pix_ctr atomics in k_trace): one launch hands out
+// shard_total = blocks of the busiest queue shard x 64 x frames positions, and each wave can
+// reserve up to 64 positions past the end of a shard before it moves on; with a bound of
+// 8 workgroups x 4 waves per CU on up to 256 CUs the over-reservation is < 2^19.
+int nr_batch_frames_per_launch(int W, int H, int band, int nshards, int shard, int nframes, int queue_shards) {
+    if (W < 1 || H < 1 || nframes < 1 || queue_shards < 1) return 0;
+    const int rows = nr_shard_rows(H, band, nshards, shard);
+    if (rows < 1) return std::min(nframes, NR_MAX_BATCH);
+    const long long nblocks = (long long)((W + 7) / 8) * ((rows + 7) / 8);
+    const long long per_frame = ((nblocks + queue_shards - 1) / queue_shards) * 64;  // busiest shard
+    const long long slop = 256ll * 8 * 4 * 64;
+    const long long cap = ((1ll << 32) - 1 - slop) / per_frame;
+    return (int)std::min<long long>(std::min(nframes, NR_MAX_BATCH), cap);
 }
 
 int nr_shard_rows(int H, int band, int nshards, int shard) {

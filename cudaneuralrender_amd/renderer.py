@@ -80,6 +80,12 @@ def shard_rows(H, band, nshards, shard):
     return lib().nr_shard_rows(H, band, nshards, shard)
 
 
+def batch_frames_per_launch(W, H, band, nshards, shard, nframes, queue_shards=8):
+    """Frames nr_render_batch puts in one k_trace launch (0: the shard overflows the
+    32-bit pixel queue even for one frame)."""
+    return lib().nr_batch_frames_per_launch(W, H, band, nshards, shard, nframes, queue_shards)
+
+
 def assemble_shards(shards, W, H, band, nshards):
     """Host re-interleave of gathered shards (list or stacked array, each padded to a
     common stride) into the full frame."""

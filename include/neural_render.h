@@ -144,6 +144,11 @@ typedef struct nr_frame {
 int nr_render_batch(nr_ctx *ctx, const nr_frame *frames, int nframes, int W, int H, int band, int nshards,
                     int shard, int max_steps, int loc, nr_stats *stats);
 int nr_shard_rows(int H, int band_rows, int nshards, int shard);
+/* Frames per k_trace launch nr_render_batch uses for this shard: min(nframes, 32), further
+ * capped so that every pixel-queue position of a launch, plus the positions its waves can
+ * over-reserve, fits the 32-bit queue counters (queue_shards = nr_set_queue_shards' n).
+ * Returns 0 when not even one frame fits (nr_render_batch then fails with NR_E_INVALID). */
+int nr_batch_frames_per_launch(int W, int H, int band_rows, int nshards, int shard, int nframes, int queue_shards);
 /* Re-interleave gathered shards (shard s's rows at src + s*stride_pixels) into a full
  * frame.  Host or device buffers (loc applies to both). */
 int nr_assemble_shards(nr_ctx *ctx, const uint32_t *src, size_t stride_pixels,

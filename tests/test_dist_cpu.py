@@ -63,7 +63,7 @@ def _worker(rank, world, port, band, W, H, nframes, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band,nframes", [(2, 8, 1), (3, 5, 1), (2, 8, 3), (3, 1, 2)])
+@pytest.mark.parametrize("world,band,nframes", [(2, 8, 1), (3, 5, 1), (2, 8, 3), (3, 1, 2), (2, 1, 3)])
 def test_gloo_gather_assemble(tmp_path, world, band, nframes):
     import torch.multiprocessing as mp
     W, H = 48, 41

@@ -75,19 +75,25 @@ def test_c3_car1_2048(rend, nets, chrome):
     assert abs(sb["ray_steps"] - s32["ray_steps"]) / s32["ray_steps"] < 0.10
 
 
-def test_c4_plane2_4096_shards(rend, nets, chrome):
-    """C4: plane_2 4096^2 bf16, rows dealt in 8-row bands to 8 shards (one per GPU in
-    the bench); the 8 shard renders re-assemble to the single-launch frame exactly."""
+@pytest.mark.parametrize("band", [1, 8])
+def test_c4_plane2_4096_shards(rend, nets, chrome, band):
+    """C4: plane_2 4096^2 bf16, rows dealt round-robin to 8 shards (one per GPU) in bands of
+    1 row (bench.py's layout) or 8; the 8 shard renders -- single-frame and through
+    nr_render_batch, bench.py's call -- re-assemble to the single-launch frame exactly."""
     setup(rend, nets, "plane_2", "bf16", chrome)
     try:
         full, st = rend.render(4096, 4096, 128)
-        shards, steps = [], 0
+        iv, nm = nr.camera(0.0, 0.0, 2.0)
+        shards, bshards, steps, bsteps = [], [], 0, 0
         for s in range(8):
-            img, sst = rend.render_shard(4096, 4096, 8, 8, s, 128)
+            img, sst = rend.render_shard(4096, 4096, band, 8, s, 128)
             shards.append(img)
             steps += sst["ray_steps"]
-        assert np.array_equal(nr.assemble_shards(shards, 4096, 4096, 8, 8), full)
-        assert steps == st["ray_steps"]
+            imgs, bst = rend.render_batch(4096, 4096, [(iv, nm, 0)] * 2, 128, band=band, nshards=8, shard=s)
+            assert np.array_equal(imgs[0], img) and np.array_equal(imgs[1], img)
+            bsteps += bst["ray_steps"]
+        assert np.array_equal(nr.assemble_shards(shards, 4096, 4096, band, 8), full)
+        assert steps == st["ray_steps"] and bsteps == 2 * st["ray_steps"]
         rend.set_precision("fp32")
         f32, s32 = rend.render(4096, 4096, 128)
     finally:

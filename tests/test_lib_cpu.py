@@ -162,3 +162,22 @@ def test_device_code_has_no_packed_fp32(tmp_path):
         assert not bad, f"{p.name}: {len(bad)} packed-FP32 instructions"
         n_mfma += len(re.findall(r"v_mfma_f32_32x32x16_(?:bf16|f16)", dis))
     assert n_mfma > 0
+
+
+def test_batch_frames_per_launch_fits_the_queue_counters():
+    """nr_render_batch caps the frames of one launch so that the busiest pixel-queue shard's
+    positions (plus the waves' over-reservation) stay below 2^32 (16384^2 x 16
+    frames on one queue shard, or 32768^2 x 32 frames on 8, used to wrap the counter)."""
+    f = nr.batch_frames_per_launch
+    assert f(1024, 1024, 1, 1, 0, 32) == 32
+    assert f(1024, 1024, 1, 1, 0, 5) == 5
+    assert f(1024, 1024, 1, 1, 0, 100) == 32
+    for W, H, q, n in [(16384, 16384, 1, 16), (32768, 32768, 8, 32), (46340, 46340, 1, 32), (8192, 8192, 8, 32)]:
+        k = f(W, H, 1, 1, 0, n, q)
+        per_frame = -(-((W + 7) // 8) * ((H + 7) // 8) // q) * 64
+        assert 1 <= k <= min(n, 32)
+        assert k * per_frame + 256 * 8 * 4 * 64 < 2 ** 32, (W, H, q, k)
+        if k < min(n, 32):
+            assert (k + 1) * per_frame + 256 * 8 * 4 * 64 >= 2 ** 32
+    assert f(16384, 16384, 1, 1, 0, 16, 1) == 15
+    assert f(0, 16, 1, 1, 0, 4) == 0

@@ -21,3 +21,4 @@ timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 "$REPO/tools/render_frames.py" --frames 3 --batch 32 > "$OUT/write.log" 2>&1
 python3 "$REPO/tools/traffic.py" "$OUT" 32 > "$OUT/traffic.json"
+cp "$OUT/traffic.json" "$REPO/gpurun_out/pmc_traffic_$TAG.json"

@@ -1,4 +1,4 @@
-"""HBM traffic per k_trace launch from tools/profile_round.sh's two --pmc passes.
+"""HBM traffic per k_trace launch (and per frame: bench.py scales it by its frames per launch) from tools/profile_round.sh's two --pmc passes.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE is reported in
 KiB and under-counts wide reads by 2x, so bytes = FETCH_SIZE * 1024 * 2; WRITE_SIZE in KiB.
@@ -37,6 +37,7 @@ print(json.dumps({
     "write_size_kb": round(write, 2),
     "correction": "bytes = FETCH_SIZE*1024*2 (gfx950 under-reports wide reads 2x) + WRITE_SIZE*1024",
     "hbm_bytes_per_launch": int(hbm),
+    "hbm_bytes_per_frame": int(hbm / max(batch, 1)),
     "algorithmic_bytes_per_launch": (1024 * 1024 * 4) * max(batch, 1) + 30 * 1024 + 1024 * 1024,
     "note": "output pixels are written 4 B at a time as rays finish (scattered), hence write > 4 MiB",
 }, indent=1))
