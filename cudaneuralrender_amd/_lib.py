@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("NR_LIBRARY") or os.path.join(_HERE, "lib", "libnr.so"
 
 NR_OK = 0
 NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}
-NR_SCENE = {"v1": 0, "tanh": 1}
+NR_SCENE = {"v1": 0, "tanh": 1, "subtract": 2, "cylinders": 3, "displace": 4, "round": 5}
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
 NR_SCHEDULE = {"persistent": 0, "wavefront": 1, "layered": 2}

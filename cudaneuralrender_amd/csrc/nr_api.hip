@@ -726,7 +726,7 @@ int nr_set_static(nr_ctx *c, int color_type, int num_inputs) {
 
 int nr_set_scene(nr_ctx *c, int scene) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    if (scene != NR_SCENE_V1 && scene != NR_SCENE_TANH) return set_err(c, NR_E_INVALID, "unknown scene %d", scene);
+    if (scene < NR_SCENE_V1 || scene > NR_SCENE_ROUND) return set_err(c, NR_E_INVALID, "unknown scene %d", scene);
     c->scene = scene;
     return NR_OK;
 }

@@ -131,6 +131,53 @@ __device__ __forceinline__ float smooth_union(float d1, float d2, float k) {  //
 // z offset of the sphere grid in frame `frame` (cP.z += ..., :184), in f64 as the reference
 __device__ __forceinline__ double sphere_zoff(int frame) { return -0.7 + ((double)(frame * 2) * 0.7 / 360.0); }
 
+// sdfOpSmoothSubtraction (:137-142): h = __saturatef(0.5 - 0.5*(d1+d2)/k);
+// mix = d1*(1.0-h) - d2*h; return mix + k*h*(1.0-h) -- the double literals promote.  As in
+// smooth_union, |d1+d2| >= k makes the f64 quotient >= 0.5 in magnitude, so h is exactly
+// 0 or 1 and only the division is skipped; the rest is the reference expression with that
+// h (CPU proof: tests/test_oracle.py::test_smooth_subtraction_kernel_form_bit_exact).
+__device__ __forceinline__ float smooth_sub_h(float d1, float d2, float k, float h) {
+    const float mix = (float)((double)d1 * (1.0 - (double)h) - (double)(d2 * h));
+    return (float)((double)mix + (double)(k * h) * (1.0 - (double)h));
+}
+__device__ __forceinline__ float smooth_subtraction(float d1, float d2, float k) {
+    const float t = d1 + d2;
+    float h;
+    if (t >= k) h = 0.0f;
+    else if (t <= -k) h = 1.0f;
+    else h = saturatef_((float)(0.5 - 0.5 * (double)t / (double)k));
+    return smooth_sub_h(d1, d2, k, h);
+}
+
+// sin from IEEE basic double operations (identical algorithm to the oracle's nr_sin_f):
+// x - k pi/2 with a two-part pi/2, then the Taylor series of sin / cos to degree 21 / 22
+// (|r| <= pi/4), rounded once to f32.  CUDA's sinf is not pinned; both sides need one
+// definition (as for tanh).
+__device__ float nr_sin(float xf) {
+    if (xf != xf) return xf;
+    if (xf == INFINITY || xf == -INFINITY) return __builtin_nanf("");
+    const double x = (double)xf;
+    const double kd = floor(x * 0.63661977236758134308 + 0.5);
+    const double r = (x - kd * 1.57079632673412561417e+00) - kd * 6.07710050650619224932e-11;
+    const double z = r * r;
+    const double sc[11] = {1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0, -1.0 / 39916800.0,
+                           1.0 / 6227020800.0, -1.0 / 1307674368000.0, 1.0 / 355687428096000.0,
+                           -1.0 / 121645100408832000.0, 1.0 / 51090942171709440000.0};
+    const double cc[12] = {1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0, -1.0 / 3628800.0,
+                           1.0 / 479001600.0, -1.0 / 87178291200.0, 1.0 / 20922789888000.0,
+                           -1.0 / 6402373705728000.0, 1.0 / 2432902008176640000.0,
+                           -1.0 / 1124000727777607680000.0};
+    double ps = sc[10], pc = cc[11];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) ps = ps * z + sc[i];
+#pragma unroll
+    for (int i = 10; i >= 0; --i) pc = pc * z + cc[i];
+    const double sn = r * ps;
+    const int q = (int)(kd - 4.0 * floor(kd * 0.25));  // k mod 4 in [0, 3]
+    const double v = q == 0 ? sn : (q == 1 ? pc : (q == 2 ? -sn : -pc));
+    return (float)v;
+}
+
 __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
@@ -164,9 +211,70 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     return s;
 }
 
+// manySphere(p, nSDF, false) (:176-196): the 9 spheres smooth-subtracted from the surface,
+// the coordinates formed as in many_sphere
+__device__ float many_sphere_sub(F3 p, float nsdf, double zoff) {
+    const float x0 = (float)((double)p.x + 0.5);
+    const float x1 = (float)((double)x0 - 0.4);
+    const float x2 = (float)((double)x1 - 0.4);
+    const float ys = (float)((double)p.y - 0.6);
+    const float y0 = (float)((double)ys + 0.4);
+    const float y1 = (float)((double)y0 + 0.4);
+    const float y2 = (float)((double)y1 + 0.4);
+    const float zc = (float)((double)p.z + zoff);
+    const float xx[3] = {x0 * x0, x1 * x1, x2 * x2};
+    const float yy[3] = {y0 * y0, y1 * y1, y2 * y2};
+    const float zz = zc * zc;
+    float s = nsdf;
+#pragma unroll
+    for (int row = 0; row < 3; ++row)
+#pragma unroll
+        for (int col = 0; col < 3; ++col) s = smooth_subtraction(s, sqrtf((xx[col] + yy[row]) + zz) - 0.1f, 0.01f);
+    return s;
+}
+
+// manyCylinderCut (:157-174): 300 cylinders (sdfCylinder :96-100, c = 0.02, infinite along
+// z) in 15 rows of 20 smooth-subtracted from the surface; cP.y starts at p.y - 0.5 and
+// every row adds 0.1 and resets cP.x = p.x + 0.9, every cylinder then steps cP.x by -0.1
+// (f64 updates of f32 coordinates, as the reference's double literals make them)
+__device__ float many_cylinder_cut(F3 p, float nsdf) {
+    float s = nsdf;
+    float cy = (float)((double)p.y - 0.5);
+    for (int row = 0; row < 15; ++row) {
+        cy = (float)((double)cy + 0.1);
+        const float dy = cy - 0.02f;
+        const float dyy = dy * dy;
+        float cx = (float)((double)p.x + 0.9);
+        for (int col = 0; col < 20; ++col) {
+            const float dx = cx - 0.02f;
+            s = smooth_subtraction(s, sqrtf(dx * dx + dyy) - 0.02f, 0.01f);
+            cx = (float)((double)cx - 0.1);
+        }
+    }
+    return s;
+}
+
+// displacementPattern (:151-154) = sdfOpDisplace(p, tanh(nSDF)) (:103-110):
+// d += sin(5 p.x) sin(5 p.y) sin(5 p.z) * 0.05 (f32 products, the 0.05 promotes)
+__device__ float displacement_pattern(F3 p, float nsdf) {
+    const float d = nr_tanh(nsdf);
+    const float w = nr_sin(5.0f * p.x) * nr_sin(5.0f * p.y) * nr_sin(5.0f * p.z);
+    return (float)((double)d + (double)w * 0.05);
+}
+
+// The scenes sceneSDF's alternatives select (:217-230), out of line so that the inlined
+// v1 / tanh paths of the march kernels keep their registers.
+__device__ __noinline__ float scene_sdf_alt(F3 p, float nsdf, int scene, double zoff) {
+    if (scene == NR_SCENE_SUBTRACT) return many_sphere_sub(p, nsdf, zoff);
+    if (scene == NR_SCENE_CYLINDERS) return many_cylinder_cut(p, nsdf);
+    if (scene == NR_SCENE_DISPLACE) return displacement_pattern(p, nsdf);
+    return nr_tanh(nsdf) - 0.04f;  // NR_SCENE_ROUND: sdfOpRound(tanh(nSDF), 0.04) (:112-115, :221)
+}
+
 __device__ __forceinline__ float scene_sdf(F3 p, float nsdf, int scene, double zoff) {  // :217-230
+    if (scene == NR_SCENE_V1) return many_sphere(p, nsdf, zoff);
     if (scene == NR_SCENE_TANH) return nr_tanh(nsdf);
-    return many_sphere(p, nsdf, zoff);
+    return scene_sdf_alt(p, nsdf, scene, zoff);
 }
 
 __device__ __forceinline__ uint32_t rgba_to_uint(float r, float g, float b, float a) {  // :266-274

@@ -42,6 +42,10 @@ extern "C" {
 /* scene composition, sceneSDF (volumeRender_kernel.cu:217-230) */
 #define NR_SCENE_V1 0        /* v1: manySphere(p, nSDF, true) -- 9-sphere smooth union (:222) */
 #define NR_SCENE_TANH 1      /* tanh(nSDF), the pure neural surface (:229) */
+#define NR_SCENE_SUBTRACT 2  /* manySphere(p, nSDF, false) -- 9 spheres smooth-subtracted (:139-142, :190-191) */
+#define NR_SCENE_CYLINDERS 3 /* manyCylinderCut(p, nSDF) -- 300 cylinders smooth-subtracted (:157-174) */
+#define NR_SCENE_DISPLACE 4  /* displacementPattern(p, nSDF) = sdfOpDisplace(p, tanh(nSDF)) (:104-110, :152-154) */
+#define NR_SCENE_ROUND 5     /* sdfOpRound(tanh(nSDF), 0.04) (:112-115, :221) */
 
 /* colouring, c_coloringType (volumeRender_kernel.cu:33) */
 #define NR_COLOR_FACING 0    /* facingColor (:380-384) */

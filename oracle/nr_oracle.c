@@ -19,7 +19,10 @@
  *       createBatch :504-547), singleMarch :416-477, surfaceNormal :361-377,
  *       matCapColor :387-413, facingColor :380-384, rgbaFloatToInt :266-274,
  *       sceneSDF :217-230 (v1: manySphere :177-196 smooth union :145-149;
- *       tanh variant :229), intersectSphere :200-215, float3 helpers
+ *       the tanh variant :229 and the alternatives the reference comments out:
+ *       manySphere subtraction :139-142/:190-191, manyCylinderCut :157-174 with
+ *       sdfCylinder :96-100, displacementPattern :151-154 with sdfOpDisplace :103-110,
+ *       sdfOpRound(tanh) :112-115/:221), intersectSphere :200-215, float3 helpers
  *       (helper_math.h dot/length/normalize :1248-1313).
  *   The loop is restated in the reference's own shape (full-image masks, an
  *   exclusive scan, a packed batch, one MLP call per iteration) so that it is
@@ -39,6 +42,7 @@
  *       other pixel.
  *   tanh the reference calls CUDA tanhf; here tanh is nr_tanh_f below, built
  *       only from IEEE basic double operations so that CPU and GPU agree bit for bit.
+ *   sin  likewise CUDA sinf (sdfOpDisplace) is nr_sin_f below.
  *   anim with numInputs == 4 the reference writes normal-estimation points with a
  *       stride of 3 (:538-545), leaving 4-input batches partly uninitialised; here
  *       every batch point is (x, y, z, frame).
@@ -262,7 +266,8 @@ float nr_tanh_f(float x)
 
 /* ------------------------------------------------------------ scene SDF */
 
-enum { OR_SCENE_V1 = 0, OR_SCENE_TANH = 1 };
+enum { OR_SCENE_V1 = 0, OR_SCENE_TANH = 1, OR_SCENE_SUBTRACT = 2, OR_SCENE_CYLINDERS = 3, OR_SCENE_DISPLACE = 4,
+       OR_SCENE_ROUND = 5 };
 
 static float sdfSphere(f3 p, float s) { return length3(p) - s; }          /* :67-71 */
 
@@ -290,10 +295,104 @@ static float manySphere(f3 p, float nSDF, int frame)                       /* :1
     return s;
 }
 
+static float sdfOpSmoothSubtraction(float d1, float d2, float k)           /* :137-142 */
+{
+    float h = saturatef((float)(0.5 - 0.5 * (double)(d1 + d2) / (double)k));
+    float mix = (float)((double)d1 * (1.0 - (double)h) - (double)(d2 * h));
+    return (float)((double)mix + (double)(k * h) * (1.0 - (double)h));
+}
+
+static float manySphereSub(f3 p, float nSDF, int frame)           /* :176-196, doUnion = false */
+{
+    float s = nSDF;
+    f3 cP = p;
+    cP.y = (float)((double)cP.y - 0.6);
+    cP.z = (float)((double)cP.z + (-0.7 + ((double)(frame * 2) * 0.7 / 360.0)));
+    for (int i = 0; i < 9; i++) {
+        if (i % 3 == 0) {
+            cP.y = (float)((double)cP.y + 0.4);
+            cP.x = (float)((double)p.x + 0.5);
+        }
+        s = sdfOpSmoothSubtraction(s, sdfSphere(cP, 0.1f), 0.01f);
+        cP.x = (float)((double)cP.x - 0.4);
+    }
+    return s;
+}
+
+static float sdfCylinder(f3 p, f3 c)                                       /* :96-100 */
+{
+    float dx = p.x - c.x, dy = p.y - c.z;       /* make_float2(p.x, p.y) - make_float2(c.x, c.z) */
+    float l = sqrtf(dx * dx + dy * dy);         /* length(float2) = sqrtf(dot(v, v)) */
+    return l - c.y;
+}
+
+static float manyCylinderCut(f3 p, float nSDF)                             /* :157-174 */
+{
+    float s = nSDF;
+    f3 c = { 0.02f, 0.02f, 0.02f };             /* make_float3(0.02) */
+    f3 cP = p;
+    cP.y = (float)((double)cP.y - 0.5);
+    for (int i = 0; i < 300; i++) {
+        if (i % 20 == 0) {
+            cP.y = (float)((double)cP.y + 0.1);
+            cP.x = (float)((double)p.x + 0.9);
+        }
+        s = sdfOpSmoothSubtraction(s, sdfCylinder(cP, c), 0.01f);
+        cP.x = (float)((double)cP.x - 0.1);
+    }
+    return s;
+}
+
+/* sin built from IEEE basic double operations (CUDA's sinf is not pinned; the GPU runs
+ * the same algorithm, nr_device.h nr_sin): x - k pi/2 with a two-part pi/2, Taylor series
+ * of sin / cos to degree 21 / 22 on |r| <= pi/4, one rounding to float. */
+float nr_sin_f(float xf)
+{
+    if (xf != xf) return xf;
+    if (xf == INFINITY || xf == -INFINITY) return NAN;
+    double x = (double)xf;
+    double kd = floor(x * 0.63661977236758134308 + 0.5);
+    double r = (x - kd * 1.57079632673412561417e+00) - kd * 6.07710050650619224932e-11;
+    double z = r * r;
+    static const double sc[11] = { 1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0,
+        -1.0 / 39916800.0, 1.0 / 6227020800.0, -1.0 / 1307674368000.0, 1.0 / 355687428096000.0,
+        -1.0 / 121645100408832000.0, 1.0 / 51090942171709440000.0 };
+    static const double cc[12] = { 1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0,
+        -1.0 / 3628800.0, 1.0 / 479001600.0, -1.0 / 87178291200.0, 1.0 / 20922789888000.0,
+        -1.0 / 6402373705728000.0, 1.0 / 2432902008176640000.0, -1.0 / 1124000727777607680000.0 };
+    double ps = sc[10], pc = cc[11];
+    for (int i = 9; i >= 0; --i) ps = ps * z + sc[i];
+    for (int i = 10; i >= 0; --i) pc = pc * z + cc[i];
+    double sn = r * ps;
+    int q = (int)(kd - 4.0 * floor(kd * 0.25));
+    double v = q == 0 ? sn : (q == 1 ? pc : (q == 2 ? -sn : -pc));
+    return (float)v;
+}
+
+static float sdfOpDisplace(f3 p, float s)                                  /* :103-110 */
+{
+    float d = s;
+    d = (float)((double)d + (double)(nr_sin_f(5 * p.x) * nr_sin_f(5 * p.y) * nr_sin_f(5 * p.z)) * 0.05);
+    return d;
+}
+
+static float displacementPattern(f3 p, float nSDF)                         /* :151-154 */
+{
+    return sdfOpDisplace(p, nr_tanh_f(nSDF));
+}
+
+static float sdfOpRound(float s, float rad) { return s - rad; }            /* :112-115 */
+
 static float sceneSDF(f3 p, float nSDF, int scene, int frame)              /* :217-230 */
 {
-    if (scene == OR_SCENE_TANH) return nr_tanh_f(nSDF);
-    return manySphere(p, nSDF, frame);
+    switch (scene) {
+    case OR_SCENE_TANH: return nr_tanh_f(nSDF);                             /* :229 */
+    case OR_SCENE_SUBTRACT: return manySphereSub(p, nSDF, frame);
+    case OR_SCENE_CYLINDERS: return manyCylinderCut(p, nSDF);               /* :223 */
+    case OR_SCENE_DISPLACE: return displacementPattern(p, nSDF);            /* :219 */
+    case OR_SCENE_ROUND: return sdfOpRound(nr_tanh_f(nSDF), 0.04f);          /* :221 */
+    default: return manySphere(p, nSDF, frame);                             /* :222 */
+    }
 }
 
 /* ------------------------------------------------------------- shading */
@@ -507,6 +606,55 @@ float or_scene_sdf(float px, float py, float pz, float nsdf, int scene, int fram
  * against the reference forms above.
  */
 float or_smooth_union_ref(float d1, float d2, float k) { return sdfOpSmoothUnion(d1, d2, k); }
+
+/* GPU form of sdfOpSmoothSubtraction (nr_device.h smooth_subtraction): the f64 division
+ * skipped when |d1 + d2| >= k, where h is exactly 0 or 1. */
+static float smooth_sub_h(float d1, float d2, float k, float h)
+{
+    float mix = (float)((double)d1 * (1.0 - (double)h) - (double)(d2 * h));
+    return (float)((double)mix + (double)(k * h) * (1.0 - (double)h));
+}
+float or_smooth_sub_ref(float d1, float d2, float k) { return sdfOpSmoothSubtraction(d1, d2, k); }
+float or_smooth_sub_kernelform(float d1, float d2, float k)
+{
+    float t = d1 + d2, h;
+    if (t >= k) h = 0.0f;
+    else if (t <= -k) h = 1.0f;
+    else h = saturatef((float)(0.5 - 0.5 * (double)t / (double)k));
+    return smooth_sub_h(d1, d2, k, h);
+}
+void or_batch_smooth_sub(const float *d1, const float *d2, long n, float k, float *ref, float *ker)
+{
+    for (long i = 0; i < n; ++i) {
+        ref[i] = or_smooth_sub_ref(d1[i], d2[i], k);
+        ker[i] = or_smooth_sub_kernelform(d1[i], d2[i], k);
+    }
+}
+/* GPU form of manyCylinderCut (nr_device.h many_cylinder_cut): rows and columns */
+static float many_cylinder_kernelform(float px, float py, float nsdf)
+{
+    float s = nsdf;
+    float cy = (float)((double)py - 0.5);
+    for (int row = 0; row < 15; ++row) {
+        cy = (float)((double)cy + 0.1);
+        float dy = cy - 0.02f, dyy = dy * dy;
+        float cx = (float)((double)px + 0.9);
+        for (int col = 0; col < 20; ++col) {
+            float dx = cx - 0.02f;
+            s = or_smooth_sub_kernelform(s, sqrtf(dx * dx + dyy) - 0.02f, 0.01f);
+            cx = (float)((double)cx - 0.1);
+        }
+    }
+    return s;
+}
+void or_batch_cylinders(const float *p, const float *nsdf, long n, float *ref, float *ker)
+{
+    for (long i = 0; i < n; ++i) {
+        f3 q = { p[3 * i], p[3 * i + 1], p[3 * i + 2] };
+        ref[i] = manyCylinderCut(q, nsdf[i]);
+        ker[i] = many_cylinder_kernelform(q.x, q.y, nsdf[i]);
+    }
+}
 
 float or_smooth_union_kernelform(float d1, float d2, float k)
 {

@@ -40,6 +40,12 @@ def lib():
         L.or_batch_smooth_union.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
         L.or_batch_many_sphere.restype = None
         L.or_batch_many_sphere.argtypes = [P, P, ctypes.c_long, I, P, P]
+        L.nr_sin_f.restype = ctypes.c_float
+        L.nr_sin_f.argtypes = [ctypes.c_float]
+        L.or_batch_smooth_sub.restype = None
+        L.or_batch_smooth_sub.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
+        L.or_batch_cylinders.restype = None
+        L.or_batch_cylinders.argtypes = [P, P, ctypes.c_long, P, P]
         L.or_batch_intersect.restype = None
         L.or_batch_intersect.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
         _lib = L
@@ -98,6 +104,28 @@ def scene_sdf(p, nsdf, scene=0, frame=0):
 
 def tanh_f(x):
     return lib().nr_tanh_f(float(x))
+
+
+def sin_f(x):
+    return lib().nr_sin_f(float(x))
+
+
+def smooth_sub_pair(d1, d2, k=0.01):
+    """(reference form, kernel form) of sdfOpSmoothSubtraction over arrays (bitwise comparable)."""
+    d1 = np.ascontiguousarray(d1, np.float32)
+    d2 = np.ascontiguousarray(d2, np.float32)
+    ref, ker = np.empty_like(d1), np.empty_like(d1)
+    lib().or_batch_smooth_sub(d1.ctypes.data, d2.ctypes.data, d1.size, k, ref.ctypes.data, ker.ctypes.data)
+    return ref, ker
+
+
+def cylinders_pair(p, nsdf):
+    """(reference form, kernel form) of manyCylinderCut over points (bitwise comparable)."""
+    p = np.ascontiguousarray(p, np.float32)
+    nsdf = np.ascontiguousarray(nsdf, np.float32)
+    ref, ker = np.empty_like(nsdf), np.empty_like(nsdf)
+    lib().or_batch_cylinders(p.ctypes.data, nsdf.ctypes.data, nsdf.size, ref.ctypes.data, ker.ctypes.data)
+    return ref, ker
 
 
 def smooth_union_pair(d1, d2, k=0.01):

@@ -86,7 +86,7 @@ def render_both(rend, K, B, W, H, steps, cam=(0.0, 0.0, 2.0), frame=0, color=1, 
         rend.set_matcap(matcap)
     img, st = rend.render(W, H, steps)
     ref, rst = oracle.OracleNet(K, B).render(W, H, iv, nm, frame=frame, color_type=color, num_inputs=ninputs,
-                                             scene=0 if scene == "v1" else 1, matcap=matcap if color else None,
+                                             scene=nr.NR_SCENE[scene], matcap=matcap if color else None,
                                              max_steps=steps)
     return img, st, ref, rst
 
@@ -147,6 +147,36 @@ def test_animation_network_four_inputs(rend, chrome):
         img, st, ref, rst = render_both(rend, K, B, 64, 48, 96, cam=(10.0, 60.0, 2.0), frame=frame, ninputs=4,
                                         matcap=chrome, scene="tanh")
         assert_same(img, st, ref, rst)
+
+
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
+@pytest.mark.parametrize("scene", ["v1", "tanh"])
+def test_fused_four_input_network(rend, chrome, schedule, scene):
+    """A [4, 32 x 8, 1] network (numInputs = 4, main.cpp:619-621; the frame number is the 4th
+    input, kernel.cu:524-545) takes the FUSED march kernels (k_trace's and k_march16's
+    4-input layer 0): single frames and one nr_render_batch of three frames equal the
+    oracle frame by frame (seeded random weights: parity unpinned against the reference)."""
+    K, B = random_net([4] + [32] * 8 + [1], 41, scale=1.4)
+    load(rend, K, B)  # [4, 32, ..., 32, 1]: a fused shape (nr_pack.cpp fused_shape_ok)
+    rend.set_schedule(schedule)
+    try:
+        iv, nm = nr.camera(-12.0, 70.0, 2.0)
+        rend.set_static(nr.NR_COLOR_MATCAP, 4).set_scene(scene).set_matcap(chrome)
+        refs = []
+        for frame in (0, 45, 300):
+            rend.set_view(iv, nm, frame)
+            img, st = rend.render(72, 56, 96)
+            ref, rst = oracle.OracleNet(K, B).render(72, 56, iv, nm, frame=frame, color_type=1, num_inputs=4,
+                                                     scene=nr.NR_SCENE[scene], matcap=chrome, max_steps=96)
+            assert_same(img, st, ref, rst)
+            assert rst["rays_hit"] > 0
+            refs.append((ref, rst))
+        imgs, bst = rend.render_batch(72, 56, [(iv, nm, f) for f in (0, 45, 300)], 96)
+        for img, (ref, rst) in zip(imgs, refs):
+            assert np.array_equal(img, ref)
+        assert bst["ray_steps"] == sum(r[1]["ray_steps"] for r in refs)
+    finally:
+        rend.set_schedule("persistent").set_static(nr.NR_COLOR_MATCAP, 3)
 
 
 @pytest.mark.parametrize("chunk", [64, 1000, 4096])

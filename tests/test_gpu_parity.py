@@ -77,6 +77,11 @@ RENDER_CASES = [
     (97, 61, "v1", "facing", 25.0, 40.0, 2.0, 64),
     (64, 64, "v1", "facing", 10.0, 300.0, 3.0, 6000),
     (1, 1, "v1", "facing", 0.0, 0.0, 2.0, 100),
+    # the scenes sceneSDF comments out (volumeRender_kernel.cu:217-229)
+    (96, 80, "subtract", "matcap", -15.0, 40.0, 2.0, 128),
+    (64, 64, "cylinders", "facing", 20.0, 30.0, 2.0, 128),
+    (96, 72, "displace", "matcap", 10.0, 200.0, 2.0, 128),
+    (96, 72, "round", "facing", -25.0, 100.0, 2.25, 128),
 ]
 
 
@@ -89,7 +94,7 @@ def test_render_bitexact(rend, nets, chrome, W, H, scene, color, rx, ry, zoom, s
     ct = nr.NR_COLOR_MATCAP if color == "matcap" else nr.NR_COLOR_FACING
     rend.set_view(iv, nm, 0).set_static(ct, 3).set_scene(scene).set_matcap(chrome)
     img, st = rend.render(W, H, steps)
-    ref, rst = oracle.OracleNet(K, B).render(W, H, iv, nm, color_type=ct, scene=0 if scene == "v1" else 1,
+    ref, rst = oracle.OracleNet(K, B).render(W, H, iv, nm, color_type=ct, scene=nr.NR_SCENE[scene],
                                              matcap=chrome if ct else None, max_steps=steps)
     diff = img != ref
     assert not diff.any(), f"{diff.sum()} pixels differ; gpu stats {st} oracle {rst}"

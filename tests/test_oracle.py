@@ -118,6 +118,60 @@ def test_smooth_union_kernel_form_bit_exact():
     assert same.all(), (d1[~same][:5], d2[~same][:5], ref[~same][:5], ker[~same][:5])
 
 
+def test_smooth_subtraction_kernel_form_bit_exact():
+    """nr_device.h evaluates sdfOpSmoothSubtraction (volumeRender_kernel.cu:137-142) without
+    the f64 division when |d1+d2| >= k (h exactly 0 or 1); bit-identical to the reference
+    form, signed zeros, infinities and NaN included."""
+    rng = np.random.default_rng(4)
+    n = 2_000_000
+    d1 = rng.standard_normal(n).astype(np.float32) * rng.choice([1e-4, 1e-2, 1.0], n).astype(np.float32)
+    d2 = -d1 + (rng.standard_normal(n) * rng.choice([1e-3, 1e-2, 1e-1], n)).astype(np.float32)
+    k = np.float32(0.01)
+    e = d1[:1000]
+    edge = np.concatenate([k - e, -k - e, np.nextafter(k - e, 0), np.nextafter(-k - e, 0)]).astype(np.float32)
+    d1 = np.concatenate([d1, e, e, e, e]).astype(np.float32)
+    d2 = np.concatenate([d2, edge]).astype(np.float32)
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e38, -1e38, 1e-45, -1e-45, 0.01, -0.01, 0.005], np.float32)
+    a, b = np.meshgrid(sp, sp)
+    d1 = np.concatenate([d1, a.ravel()]).astype(np.float32)
+    d2 = np.concatenate([d2, b.ravel()]).astype(np.float32)
+    ref, ker = oracle.smooth_sub_pair(d1, d2, 0.01)
+    same = (ref.view(np.uint32) == ker.view(np.uint32)) | (np.isnan(ref) & np.isnan(ker))
+    assert same.all(), (d1[~same][:5], d2[~same][:5], ref[~same][:5], ker[~same][:5])
+
+
+def test_many_cylinder_kernel_form_bit_exact():
+    """manyCylinderCut (volumeRender_kernel.cu:157-174) walked as 15 rows x 20 columns, as the
+    kernel evaluates it; points near the cylinder shells take the smooth-subtraction slow path."""
+    rng = np.random.default_rng(6)
+    n = 60_000
+    p = rng.uniform(-1.3, 1.3, size=(n, 3)).astype(np.float32)
+    # near the axes: x = -0.88 + 0.1 i + 0.02..., y = -0.38 + 0.1 j + 0.02
+    i = rng.integers(0, 20, n // 2)
+    j = rng.integers(0, 15, n // 2)
+    ang = rng.uniform(0, 2 * np.pi, n // 2)
+    rad = 0.02 + rng.normal(0, 0.01, n // 2)
+    p[: n // 2, 0] = (-0.9 + 0.1 * i + 0.02 + rad * np.cos(ang)).astype(np.float32)
+    p[: n // 2, 1] = (0.5 - 0.1 - 0.1 * j + 0.02 + rad * np.sin(ang)).astype(np.float32)
+    nsdf = rng.normal(0, 0.3, n).astype(np.float32)
+    ref, ker = oracle.cylinders_pair(p, nsdf)
+    same = (ref.view(np.uint32) == ker.view(np.uint32)) | (np.isnan(ref) & np.isnan(ker))
+    assert same.all(), (p[~same][:3], ref[~same][:3], ker[~same][:3])
+    assert (ref != nsdf).mean() > 0.05  # the cylinders actually cut
+
+
+def test_sin_restatement_close_to_libm():
+    """nr_sin_f (the sin of sdfOpDisplace, :103-110, built from IEEE double operations on CPU
+    and GPU alike) is within 1 ulp of the correctly rounded sin on the scene's range."""
+    xs = np.concatenate([np.linspace(-8, 8, 40001), np.geomspace(1e-9, 8, 3000), -np.geomspace(1e-9, 8, 3000),
+                         [0.0, -0.0]]).astype(np.float32)
+    got = np.array([oracle.sin_f(x) for x in xs], np.float32)
+    ref = np.sin(xs.astype(np.float64)).astype(np.float32)
+    ulps = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 1
+    assert np.isnan(oracle.sin_f(float("inf"))) and np.isnan(oracle.sin_f(float("nan")))
+
+
 @pytest.mark.parametrize("frame", [0, 7, 359])
 def test_many_sphere_kernel_form_bit_exact(frame):
     """manySphere (volumeRender_kernel.cu:176-196) with the sphere-grid coordinates hoisted
