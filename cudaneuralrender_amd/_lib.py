@@ -27,6 +27,8 @@ EXPORTS = [
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
     "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
+    "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
+    "nr_h5_dims", "nr_h5_read_f32",
 ]
 
 
@@ -115,6 +117,15 @@ def lib():
         "nr_layer_forward": (I, [P, I, P, P, L64, I]),
         "nr_camera": (I, [F, F, F, F, F, FP, FP]),
         "nr_h5_read_keras": (I, [ctypes.c_char_p, I, IP, IP, FP, ctypes.c_size_t]),
+        "nr_h5_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
+        "nr_h5_close": (None, [P]),
+        "nr_h5_root": (I, [P, ctypes.POINTER(ctypes.c_uint64)]),
+        "nr_h5_object_type": (I, [P, ctypes.c_uint64, IP]),
+        "nr_h5_num_members": (I, [P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_size_t)]),
+        "nr_h5_member": (I, [P, ctypes.c_uint64, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                             ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_uint64)]),
+        "nr_h5_dims": (I, [P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), I, IP]),
+        "nr_h5_read_f32": (I, [P, ctypes.c_uint64, FP, ctypes.c_size_t]),
         "nr_png_load": (I, [ctypes.c_char_p, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)), IP, IP]),
         "nr_png_save": (I, [ctypes.c_char_p, P, I, I, I]),
         "nr_ppm_save": (I, [ctypes.c_char_p, P, I, I]),

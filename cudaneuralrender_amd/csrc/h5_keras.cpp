@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -140,40 +142,46 @@ bool group_members(const File &f, uint64_t oh, std::vector<Entry> &out) {
 
 bool is_dataset(const File &f, uint64_t oh) { return find(object_messages(f, oh), 0x08) != nullptr; }
 
-// Reads a float dataset; returns its dims.
-std::vector<uint64_t> read_dataset(const File &f, uint64_t oh, std::vector<float> &vals) {
+// A float dataset's shape and where its values are.
+struct DsInfo {
+    std::vector<uint64_t> dims;
+    uint64_t count = 1, data_off = 0;
+    uint32_t esz = 4;
+    bool be = false, undefined = false;
+};
+
+DsInfo dataset_info(const File &f, uint64_t oh) {
     auto ms = object_messages(f, oh);
     const Msg *sp = find(ms, 0x01), *ty = find(ms, 0x03), *lay = find(ms, 0x08);
     if (!sp || !ty || !lay) fail(NR_E_FORMAT, "HDF5: dataset lacks dataspace/datatype/layout");
     if (ty->flags & 0x02) fail(NR_E_FORMAT, "HDF5: shared (committed) datatypes unsupported");
     if (find(ms, 0x0B)) fail(NR_E_FORMAT, "HDF5: filtered datasets unsupported");
+    DsInfo I;
     // dataspace
     int sv = f.d[sp->off], nd = f.d[sp->off + 1];
     uint64_t dp = (sv == 1) ? sp->off + 8 : (sv == 2 ? sp->off + 4 : 0);
     if (!dp) fail(NR_E_FORMAT, "HDF5: unknown dataspace version");
-    std::vector<uint64_t> dims(nd);
-    uint64_t count = 1;
-    for (int i = 0; i < nd; ++i) { dims[i] = f.uint(dp + (uint64_t)i * f.sl, f.sl); count *= dims[i]; }
+    I.dims.resize(nd);
+    for (int i = 0; i < nd; ++i) { I.dims[i] = f.uint(dp + (uint64_t)i * f.sl, f.sl); I.count *= I.dims[i]; }
     // datatype
     int cls = f.d[ty->off] & 0x0f;
     uint8_t bits0 = f.d[ty->off + 1];
-    uint32_t esz = (uint32_t)f.uint(ty->off + 4, 4);
-    if (cls != 1 || (esz != 4 && esz != 8)) fail(NR_E_FORMAT, "HDF5: dataset is not IEEE float32/float64");
-    bool be = bits0 & 1;
+    I.esz = (uint32_t)f.uint(ty->off + 4, 4);
+    if (cls != 1 || (I.esz != 4 && I.esz != 8)) fail(NR_E_FORMAT, "HDF5: dataset is not IEEE float32/float64");
+    I.be = bits0 & 1;
     // layout
     int lv = f.d[lay->off];
-    uint64_t data_off = 0, data_len = count * esz;
-    bool undefined = false;
+    const uint64_t data_len = I.count * I.esz;
     if (lv == 3 || lv == 4) {
         int lc = f.d[lay->off + 1];
         if (lc == 1) {
             uint64_t a = f.addr(lay->off + 2);
-            undefined = f.undef(a);
-            data_off = f.abs(a);
+            I.undefined = f.undef(a);
+            I.data_off = f.abs(a);
         } else if (lc == 0) {
             uint64_t n = f.uint(lay->off + 2, 2);
             if (n < data_len) fail(NR_E_FORMAT, "HDF5: compact dataset too small");
-            data_off = lay->off + 4;
+            I.data_off = lay->off + 4;
         } else {
             fail(NR_E_FORMAT, "HDF5: chunked/virtual datasets unsupported");
         }
@@ -181,27 +189,40 @@ std::vector<uint64_t> read_dataset(const File &f, uint64_t oh, std::vector<float
         int lnd = f.d[lay->off + 1], lc = f.d[lay->off + 2];
         if (lc == 1) {
             uint64_t a = f.addr(lay->off + 8);
-            undefined = f.undef(a);
-            data_off = f.abs(a);
+            I.undefined = f.undef(a);
+            I.data_off = f.abs(a);
         } else if (lc == 0) {
-            data_off = lay->off + 8 + (uint64_t)lnd * 4 + 4;
+            I.data_off = lay->off + 8 + (uint64_t)lnd * 4 + 4;
         } else {
             fail(NR_E_FORMAT, "HDF5: chunked datasets unsupported");
         }
     } else {
         fail(NR_E_FORMAT, "HDF5: unknown layout message version");
     }
-    vals.assign(count, 0.0f);
-    if (undefined) return dims;  // never written: fill value 0
-    f.need(data_off, data_len);
-    for (uint64_t i = 0; i < count; ++i) {
-        uint8_t b[8];
-        memcpy(b, &f.d[data_off + i * esz], esz);
-        if (be) std::reverse(b, b + esz);
-        if (esz == 4) { float v; memcpy(&v, b, 4); vals[i] = v; }
-        else { double v; memcpy(&v, b, 8); vals[i] = (float)v; }
+    if (!I.undefined) f.need(I.data_off, data_len);
+    return I;
+}
+
+// Reads a float dataset's values (as float) into out[0, count); returns its dims.
+void read_values(const File &f, const DsInfo &I, float *out) {
+    if (I.undefined) {  // never written: fill value 0
+        std::fill(out, out + I.count, 0.0f);
+        return;
     }
-    return dims;
+    for (uint64_t i = 0; i < I.count; ++i) {
+        uint8_t b[8];
+        memcpy(b, &f.d[I.data_off + i * I.esz], I.esz);
+        if (I.be) std::reverse(b, b + I.esz);
+        if (I.esz == 4) { float v; memcpy(&v, b, 4); out[i] = v; }
+        else { double v; memcpy(&v, b, 8); out[i] = (float)v; }
+    }
+}
+
+std::vector<uint64_t> read_dataset(const File &f, uint64_t oh, std::vector<float> &vals) {
+    const DsInfo I = dataset_info(f, oh);
+    vals.assign(I.count, 0.0f);
+    read_values(f, I, vals.data());
+    return I.dims;
 }
 
 void open_file(const char *path, File &f) {
@@ -233,6 +254,13 @@ void open_file(const char *path, File &f) {
     if (f.base == 0) f.base = sb;
 }
 
+uint64_t root_object(const File &f) {
+    // the root symbol-table entry follows the 4 addresses of the superblock
+    const int ver = f.d[f.sb + 8];
+    const uint64_t rootent = f.sb + 24 + (ver == 1 ? 4 : 0) + 4 * (uint64_t)f.so;
+    return f.addr(rootent + f.so);
+}
+
 }  // namespace
 
 // Reads a Keras Dense stack the way NeuralNetwork::load does (neuralNetwork.cpp:85-151).
@@ -241,11 +269,7 @@ int h5_read_keras(const char *path, std::vector<int> &dims, std::vector<std::vec
     try {
         File f;
         open_file(path, f);
-        // root symbol-table entry follows the 4 addresses of the superblock
-        uint64_t sb = f.sb;
-        int ver = f.d[sb + 8];
-        uint64_t rootent = sb + 24 + (ver == 1 ? 4 : 0) + 4 * (uint64_t)f.so;
-        uint64_t root_oh = f.addr(rootent + f.so);
+        const uint64_t root_oh = root_object(f);
         std::vector<Entry> layers;
         if (!group_members(f, root_oh, layers)) fail(NR_E_FORMAT, "HDF5: root is not a group");
         dims.clear(); kernels.clear(); biases.clear();
@@ -285,3 +309,117 @@ int h5_read_keras(const char *path, std::vector<int> &dims, std::vector<std::vec
 }
 
 }  // namespace nr
+
+// ---- HDF5 object tree (C ABI, neural_render.h nr_h5_*): what the HighFive subset in
+// include/highfive/ wraps.  Objects are named by their object-header addresses.
+struct nr_h5_file {
+    nr::File f;
+    uint64_t root = 0;
+    std::map<uint64_t, std::vector<nr::Entry>> members;  // group -> members, name order
+};
+
+namespace {
+const std::vector<nr::Entry> &members_of(nr_h5_file *h, uint64_t g) {
+    auto it = h->members.find(g);
+    if (it != h->members.end()) return it->second;
+    std::vector<nr::Entry> m;
+    if (!nr::group_members(h->f, g, m)) nr::fail(NR_E_INVALID, "HDF5: object is not a group");
+    return h->members.emplace(g, std::move(m)).first->second;
+}
+}  // namespace
+
+extern "C" {
+
+int nr_h5_open(const char *path, nr_h5_file **out) {
+    if (!path || !out) return nr::report_error(NR_E_INVALID, "nr_h5_open: NULL argument");
+    *out = nullptr;
+    nr_h5_file *h = new (std::nothrow) nr_h5_file;
+    if (!h) return nr::report_error(NR_E_NOMEM, "out of host memory");
+    try {
+        nr::open_file(path, h->f);
+        h->root = nr::root_object(h->f);
+        members_of(h, h->root);  // the root must be a symbol-table group
+    } catch (const nr::H5Error &e) {
+        delete h;
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    *out = h;
+    return NR_OK;
+}
+
+void nr_h5_close(nr_h5_file *h) { delete h; }
+
+int nr_h5_root(const nr_h5_file *h, uint64_t *obj) {
+    if (!h || !obj) return nr::report_error(NR_E_INVALID, "nr_h5_root: NULL argument");
+    *obj = h->root;
+    return NR_OK;
+}
+
+int nr_h5_object_type(nr_h5_file *h, uint64_t obj, int *type) {
+    if (!h || !type) return nr::report_error(NR_E_INVALID, "nr_h5_object_type: NULL argument");
+    try {
+        const auto ms = nr::object_messages(h->f, obj);
+        *type = nr::find(ms, 0x11) ? NR_H5_GROUP : (nr::find(ms, 0x08) ? NR_H5_DATASET : NR_H5_OTHER);
+    } catch (const nr::H5Error &e) {
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    return NR_OK;
+}
+
+int nr_h5_num_members(nr_h5_file *h, uint64_t group, size_t *n) {
+    if (!h || !n) return nr::report_error(NR_E_INVALID, "nr_h5_num_members: NULL argument");
+    try {
+        *n = members_of(h, group).size();
+    } catch (const nr::H5Error &e) {
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    return NR_OK;
+}
+
+int nr_h5_member(nr_h5_file *h, uint64_t group, size_t i, char *name, size_t cap, size_t *name_len, uint64_t *obj) {
+    if (!h) return nr::report_error(NR_E_INVALID, "nr_h5_member: NULL file");
+    try {
+        const auto &m = members_of(h, group);
+        if (i >= m.size()) return nr::report_error(NR_E_INVALID, "nr_h5_member: index %zu of %zu members", i, m.size());
+        if (name_len) *name_len = m[i].name.size();
+        if (obj) *obj = m[i].oh;
+        if (name) {
+            if (cap < m[i].name.size() + 1) return nr::report_error(NR_E_INVALID, "nr_h5_member: name buffer too small");
+            memcpy(name, m[i].name.c_str(), m[i].name.size() + 1);
+        }
+    } catch (const nr::H5Error &e) {
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    return NR_OK;
+}
+
+int nr_h5_dims(nr_h5_file *h, uint64_t dataset, uint64_t *dims, int cap, int *ndims) {
+    if (!h || !ndims) return nr::report_error(NR_E_INVALID, "nr_h5_dims: NULL argument");
+    try {
+        const nr::DsInfo I = nr::dataset_info(h->f, dataset);
+        *ndims = (int)I.dims.size();
+        if (dims) {
+            if (cap < (int)I.dims.size()) return nr::report_error(NR_E_INVALID, "nr_h5_dims: dims buffer too small");
+            for (size_t k = 0; k < I.dims.size(); ++k) dims[k] = I.dims[k];
+        }
+    } catch (const nr::H5Error &e) {
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    return NR_OK;
+}
+
+int nr_h5_read_f32(nr_h5_file *h, uint64_t dataset, float *out, size_t count) {
+    if (!h || (count && !out)) return nr::report_error(NR_E_INVALID, "nr_h5_read_f32: NULL argument");
+    try {
+        const nr::DsInfo I = nr::dataset_info(h->f, dataset);
+        if (count != I.count)
+            return nr::report_error(NR_E_INVALID, "nr_h5_read_f32: dataset has %llu elements, buffer %zu",
+                                    (unsigned long long)I.count, count);
+        nr::read_values(h->f, I, out);
+    } catch (const nr::H5Error &e) {
+        return nr::report_error(e.code, "%s", e.msg.c_str());
+    }
+    return NR_OK;
+}
+
+}  // extern "C"

@@ -44,6 +44,8 @@ struct nr_ctx {
     uint16_t *d_lp16 = nullptr;
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
+    bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
+    bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16 on the same pack
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
     int debug = 0;
@@ -135,6 +137,20 @@ int spread_for(const nr_ctx *c, int nframes, size_t npix) {
     return (size_t)nframes * npix >= ((size_t)8 << 20) ? 0 : 16;
 }
 
+}  // namespace
+
+int nr::report_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+namespace {
+
 #define HIPCHK(ctx, expr)                                                                            \
     do {                                                                                             \
         hipError_t e_ = (expr);                                                                      \
@@ -176,11 +192,15 @@ int upload_pack(nr_ctx *c, const std::vector<uint16_t> &a, const std::vector<flo
 int upload_lowp(nr_ctx *c) {
     dfree(c->d_lp16); dfree(c->d_lpf16);
     c->mlp16.lp = nullptr; c->mlp16.lpf = nullptr; c->mlp16.lp_bytes = 0; c->mlp16.lpf_bytes = 0;
+    c->mlp16.lp_clamp = 0;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
-    if (!pack_lowp_32(c->dims, c->kernels, c->biases, c->precision, a, f))
+    int clamp = 0;
+    if (!pack_lowp_32(c->dims, c->kernels, c->biases, c->precision, a, f, &clamp))
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
+    c->clamp_ok = clamp != 0;
+    c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp;
     return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
 }
 
@@ -287,6 +307,19 @@ int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
 // Per-frame arguments of a batch: pinned staging (reused only once the previous upload
 // has been consumed) + device copy.  With host outputs the frames of one launch go
 // through d_bout (`chunk` frames).
+// The MLP arguments of a launch over these frame numbers: the bf16 clamped-ReLU form
+// (nr_mlp16.h) needs every network input within LP_INPUT_BOUND.  Ray positions stay inside
+// the bounding sphere; the 4th input of an animation network is the frame number, checked here.
+MlpArgs mlp_for_frames(const nr_ctx *c, const nr_frame *frames, int nframes, int frame) {
+    MlpArgs M = c->mlp16;
+    if (M.in0 == 4) {
+        bool ok = std::fabs((float)frame) <= LP_INPUT_BOUND;
+        for (int i = 0; i < nframes && ok; ++i) ok = std::fabs((float)frames[i].frame) <= LP_INPUT_BOUND;
+        if (!ok) M.lp_clamp = 0;
+    }
+    return M;
+}
+
 int upload_frames(nr_ctx *c, const nr_frame *frames, int nframes, size_t npix, int loc, int chunk, hipStream_t s) {
     if (!c->ev_frames) HIPCHK(c, hipEventCreateWithFlags(&c->ev_frames, hipEventDisableTiming));
     HIPCHK(c, hipEventSynchronize(c->ev_frames));
@@ -367,7 +400,7 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
             Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
             Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
             if ((rc = prof_begin(c, 1, s)) != NR_OK) return rc;
-            HIPCHK(c, launch_march16(A, c->mlp16, Q, F, c->precision, it, grid, s));
+            HIPCHK(c, launch_march16(A, mlp_for_frames(c, frames, nframes, 0), Q, F, c->precision, it, grid, s));
             if ((rc = prof_end(c, s)) != NR_OK) return rc;
             ++tot.launches;
             if (c->check_every > 0 && (it + 1) % c->check_every == 0 && it + 1 < max_steps) {
@@ -842,7 +875,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         if (grid < 1) grid = 1;
         int rc2;
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
-        HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
+        HIPCHK(c, launch_trace(A, mlp_for_frames(c, frames, nframes, 0), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         ++launches;
         if (loc != NR_DEVICE)
@@ -1004,14 +1037,14 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             Ap.max_steps = std::min(max_steps, c->probe_steps);
             const long pwaves = ((long)T.nblocks + P.take - 1) / P.take;
             const int pgrid = (int)std::max<long>(1, std::min<long>((pwaves + 3) / 4, grid));
-            HIPCHK(c, launch_trace(Ap, c->mlp16, P, c->precision, pgrid, s));
+            HIPCHK(c, launch_trace(Ap, mlp_for_frames(c, nullptr, 0, A.frame), P, c->precision, pgrid, s));
             HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur], T.nblocks, T.bw, c->probe_dilate, s));
             if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
             T.order = c->d_order[c->order_cur];
         }
         if (T.bcost) HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
-        HIPCHK(c, launch_trace(A, c->mlp16, T, c->precision, grid, s));
+        HIPCHK(c, launch_trace(A, mlp_for_frames(c, nullptr, 0, A.frame), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         if (c->temporal) {  // order for the next frame of the same configuration
             HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, 0, s));
@@ -1247,6 +1280,8 @@ int nr_set_occupancy(nr_ctx *c, int blocks_per_cu) {
 int nr_set_debug(nr_ctx *c, int flags) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
     c->debug = flags;
+    c->no_clamp = (flags >> 9) & 1;
+    c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     return NR_OK;
 }
 

@@ -22,6 +22,8 @@ int h5_read_keras(const char *path, std::vector<int> &dims, std::vector<std::vec
 int png_decode(const char *path, std::vector<uint32_t> &rgba, int &w, int &h, std::string &err);
 int png_encode(const char *path, const uint32_t *rgba, int w, int h, int flip, std::string &err);
 int ppm_encode(const char *path, const uint32_t *rgba, int w, int h, std::string &err);
+// Records the calling thread's last error (nr_last_error(NULL)) and returns code.
+int report_error(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 
 // ---- packed network layouts (nr_pack.cpp) ----
 // fp32 16-point-tile layout (nr_mlp16.h), in floats.  Lane (j, g) of a wave = row /
@@ -58,6 +60,9 @@ constexpr int LP32_HSTRIDE = 1024;
 NR_HD constexpr inline int lp32_final(int nh) { return LP32_HID + nh * LP32_HSTRIDE; }
 NR_HD constexpr inline int lp32_elems(int nh) { return lp32_final(nh) + 32; }
 NR_HD constexpr inline int lp32_floats(int nh) { return 32 + 32 * nh + 4; }
+// bf16 clamped-ReLU pack: every network input within +-LP_INPUT_BOUND keeps every scaled
+// activation at or below 1/4 (interval bounds, nr_pack.cpp pack_lowp_32)
+constexpr float LP_INPUT_BOUND = 1048576.0f;
 
 bool fused_shape_ok(const std::vector<int> &dims);
 // Keras kernels (in x out, row-major) -> packs.  Return false if the shape is not
@@ -66,7 +71,7 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
                   const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
 bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, int precision,
-                  std::vector<uint16_t> &a_ops, std::vector<float> &bias);
+                  std::vector<uint16_t> &a_ops, std::vector<float> &bias, int *clamp = nullptr);
 
 // ---- camera (nr_camera.cpp) ----
 void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]);

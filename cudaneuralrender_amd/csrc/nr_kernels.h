@@ -12,6 +12,8 @@ struct MlpArgs {
     const float *lpf;       // float side of the low-precision pack
     int pk_bytes, lp_bytes, lpf_bytes;
     int in0, nh;
+    int lp_clamp;           // bf16 pack scaled for the clamped ReLU (nr_pack.cpp): valid for
+                            // inputs within LP_INPUT_BOUND; the launch clears it otherwise
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
@@ -97,7 +99,6 @@ struct TraceArgs {
     int nframes;                  // diagnostics: write each pixel's iteration count instead of its colour
 };
 
-int smem_bytes(const MlpArgs &M, int prec);
 int dense_lds_bytes(int in, int out);
 hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
 hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,

@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void k_init_f(RenderArgs A, const FrameArgs *_
 template <int PREC>
 __global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueArgs Q, const FrameArgs *__restrict__ F,
                                                  int it) {
-    Smem16 S = stage16(M, PREC);
+    Smem16 S = stage16<PREC, false>(M);
     const int wv = threadIdx.x >> 6;
     const long U = seg_units(Q.cnt_in, 256);
     for (long u = blockIdx.x; u < U; u += gridDim.x) {
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueA
         const long rem = n_s - (off + 64 * wv);
         const uint32_t tmask = rem >= 64 ? 0xfu : (rem <= 0 ? 0u : (1u << ((rem + 15) >> 4)) - 1u);
         float sdf = 0.0f;
-        if (tmask) sdf = mlp16(M, S.s32, S.slp, S.sfl, PREC, F[f].frame_f, sp.x, sp.y, sp.z, tmask);
+        if (tmask) sdf = mlp16(M, S.s32, S.slp, S.sfl, PREC, F[f].frame_f, sp.x, sp.y, sp.z, tmask, M.lp_clamp != 0);
         march_rays(A, seg_view(Q, s), it, live, sp, sd, sdf, F[f].zoff);
     }
 }
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueA
 // surfaceNormal + colour for the converged rays of the queue's frames: 16 rays x 4
 // tetrahedron points per wave, one fp32 4-tile mlp16 pass.
 __global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, QueueArgs Q, const FrameArgs *__restrict__ F) {
-    Smem16 S = stage16(M, NR_PRECISION_FP32);
+    Smem16 S = stage16<NR_PRECISION_FP32, true>(M);
     const int lane = lane_id(), q = lane & 3;
     const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
@@ -554,9 +554,6 @@ __global__ void k_assemble(const uint32_t *__restrict__ src, size_t stride, uint
 }
 
 // ---------------------------------------------------------- launchers
-int smem_bytes(const MlpArgs &M, int prec) {
-    return M.pk_bytes + (prec != NR_PRECISION_FP32 ? M.lp_bytes + M.lpf_bytes : 0);
-}
 
 int dense_lds_bytes(int in, int out) {
     const long b = (long)out * (in + 1) * 4;
@@ -614,7 +611,7 @@ hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArg
 }
 hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
                           int it, int grid, hipStream_t st) {
-    const int sm = smem_bytes(M, prec);
+    const int sm = smem16_bytes(M, prec, false);
     if (prec == NR_PRECISION_BF16)
         hipLaunchKernelGGL(k_march16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
     else if (prec == NR_PRECISION_FP16)
@@ -625,7 +622,7 @@ hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs
 }
 hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int grid,
                           hipStream_t st) {
-    hipLaunchKernelGGL(k_shade16, dim3(grid), dim3(256), smem_bytes(M, NR_PRECISION_FP32), st, A, M, Q, F);
+    hipLaunchKernelGGL(k_shade16, dim3(grid), dim3(256), smem16_bytes(M, NR_PRECISION_FP32, true), st, A, M, Q, F);
     return hipGetLastError();
 }
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,

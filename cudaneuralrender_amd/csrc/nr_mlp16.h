@@ -226,8 +226,75 @@ __device__ __forceinline__ f32x16 load_bias16(const float *b) {
     return f32x16{a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
 }
 
+// bf16 ReLU folded into the conversion: v_cvt_pk_bf16_f32 with the VOP3 clamp bit clamps to
+// [0, 1] (-0 and NaN -> +0; tools/cvt_clamp_probe.hip), which is the ReLU wherever the value is
+// below 1.  The clamped pack (nr_pack.cpp, M.lp_clamp) scales every layer by a power of two so
+// that, for inputs within LP_INPUT_BOUND, no activation exceeds 1/4: the scaling is exact in
+// bf16 / f32 (same exponent range), so clamp(cvt(x)) here equals max(cvt(x), 0) of relu_pack8
+// on the same pack, bit for bit -- 8 instead of 16 VALU per tile and layer.
+// No builtin sets that bit on the bf16 conversion (hipcc folds it only into v_cvt_pk_f16_f32),
+// so this is inline asm, which the compiler's hazard recognizer does not see.  It is made safe
+// by construction:
+//   * the block takes a VALU "touch" of every accumulator it converts as an input, and the
+//     compiler puts the MFMA -> VALU wait states before each touch; when the block starts,
+//     every MFMA this wave issued for these tiles has completed and none of the wave's MFMAs
+//     is in flight (the next ones consume the block's outputs), so no MFMA RAW/WAW/WAR
+//     hazard can involve a register the block reads or writes;
+//   * it ends with s_nop 1: the two wait states a VALU write needs before an MFMA reads it.
+// Outputs are early-clobber so that they never share a register with an input.
+#define NR_CVC(o, a, b) "v_cvt_pk_bf16_f32 %" #o ", %" #a ", %" #b " clamp\n"
+__device__ __forceinline__ void relu_clamp_bf16_x2(const f32x16 &c, const f32x16 &d, u32x4 (&k)[2][2]) {
+    const uint32_t t0 = __float_as_uint(c[0]) & 1u, t1 = __float_as_uint(d[0]) & 1u;  // the touches
+    asm(NR_CVC(0, 16, 17) NR_CVC(1, 18, 19) NR_CVC(2, 20, 21) NR_CVC(3, 22, 23)
+        NR_CVC(4, 24, 25) NR_CVC(5, 26, 27) NR_CVC(6, 28, 29) NR_CVC(7, 30, 31)
+        NR_CVC(8, 32, 33) NR_CVC(9, 34, 35) NR_CVC(10, 36, 37) NR_CVC(11, 38, 39)
+        NR_CVC(12, 40, 41) NR_CVC(13, 42, 43) NR_CVC(14, 44, 45) NR_CVC(15, 46, 47)
+        "s_nop 1"
+        : "=&v"(k[0][0][0]), "=&v"(k[0][0][1]), "=&v"(k[0][0][2]), "=&v"(k[0][0][3]),
+          "=&v"(k[0][1][0]), "=&v"(k[0][1][1]), "=&v"(k[0][1][2]), "=&v"(k[0][1][3]),
+          "=&v"(k[1][0][0]), "=&v"(k[1][0][1]), "=&v"(k[1][0][2]), "=&v"(k[1][0][3]),
+          "=&v"(k[1][1][0]), "=&v"(k[1][1][1]), "=&v"(k[1][1][2]), "=&v"(k[1][1][3])
+        : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
+          "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15]),
+          "v"(d[0]), "v"(d[1]), "v"(d[2]), "v"(d[3]), "v"(d[4]), "v"(d[5]), "v"(d[6]), "v"(d[7]),
+          "v"(d[8]), "v"(d[9]), "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15]),
+          "v"(t0), "v"(t1));
+}
+__device__ __forceinline__ void relu_clamp_bf16_x1(const f32x16 &c, u32x4 (&k)[2]) {
+    const uint32_t t0 = __float_as_uint(c[0]) & 1u;
+    asm(NR_CVC(0, 8, 9) NR_CVC(1, 10, 11) NR_CVC(2, 12, 13) NR_CVC(3, 14, 15)
+        NR_CVC(4, 16, 17) NR_CVC(5, 18, 19) NR_CVC(6, 20, 21) NR_CVC(7, 22, 23)
+        "s_nop 1"
+        : "=&v"(k[0][0]), "=&v"(k[0][1]), "=&v"(k[0][2]), "=&v"(k[0][3]),
+          "=&v"(k[1][0]), "=&v"(k[1][1]), "=&v"(k[1][2]), "=&v"(k[1][3])
+        : "v"(c[0]), "v"(c[1]), "v"(c[2]), "v"(c[3]), "v"(c[4]), "v"(c[5]), "v"(c[6]), "v"(c[7]),
+          "v"(c[8]), "v"(c[9]), "v"(c[10]), "v"(c[11]), "v"(c[12]), "v"(c[13]), "v"(c[14]), "v"(c[15]),
+          "v"(t0));
+}
+#undef NR_CVC
+
+// ReLU'd 16-bit B operands of both k-steps of every tile: k[t][s]
+template <int PREC, int NT, bool CL>
+__device__ __forceinline__ void relu_pack_tiles(const f32x16 (&acc)[NT], typename Lowp<PREC>::v8 (&k)[NT][2]) {
+    typedef typename Lowp<PREC>::v8 v8;
+    if constexpr (CL && PREC == NR_PRECISION_BF16) {
+        u32x4 u[NT][2];
+        if constexpr (NT == 2) relu_clamp_bf16_x2(acc[0], acc[1], u);
+        else relu_clamp_bf16_x1(acc[0], u[0]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) k[t][s] = __builtin_bit_cast(v8, u[t][s]);
+    } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) k[t][s] = relu_pack8<PREC>(acc[t], s);
+    }
+}
+
 // one hidden layer on NT tiles: acc <- W relu(acc) + b
-template <int PREC, int NT>
+template <int PREC, int NT, bool CL>
 __device__ __forceinline__ void hidden32(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int jl,
                                          f32x16 (&acc)[NT]) {
     typedef typename Lowp<PREC>::v8 v8;
@@ -235,14 +302,15 @@ __device__ __forceinline__ void hidden32(const uint16_t *__restrict__ lp, const 
     const v8 *A = reinterpret_cast<const v8 *>(lp + LP32_HID + jl * LP32_HSTRIDE);
     const v8 a0 = A[lane], a1 = A[64 + lane];
     const f32x16 bj = load_bias16(fl + 32 + 32 * jl + 16 * h);
+    v8 k[NT][2];
+    relu_pack_tiles<PREC, NT, CL>(acc, k);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const v8 k0 = relu_pack8<PREC>(acc[t], 0), k1 = relu_pack8<PREC>(acc[t], 1);
-        acc[t] = mfma32<PREC>(a1, k1, mfma32<PREC>(a0, k0, bj));
-    }
+    for (int t = 0; t < NT; ++t) acc[t] = mfma32<PREC>(a1, k[t][1], mfma32<PREC>(a0, k[t][0], bj));
 }
 
-template <int PREC, int NT, int NH>
+// CL: ReLU by the conversion's clamp (bf16 with the clamped pack, inputs within
+// LP_INPUT_BOUND -- the caller checks); otherwise cvt + v_pk_max_i16 (any pack, any input)
+template <int PREC, int NT, int NH, bool CL>
 __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh_rt, float fr, float x, float y, float z) {
     typedef typename Lowp<PREC>::e e16;
@@ -276,9 +344,9 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
     }
     if constexpr (NH > 0) {
 #pragma unroll
-        for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT>(lp, fl, jl, acc);
+        for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT, CL>(lp, fl, jl, acc);
     } else {
-        for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT>(lp, fl, jl, acc);
+        for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT, CL>(lp, fl, jl, acc);
     }
     // final layer: row 0 of A (lanes 0 and 32) holds the weights, every other row is 0;
     // the accumulator starts at 0 and the bias is added to register 0 alone
@@ -289,36 +357,54 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
         f1 = reinterpret_cast<const v8 *>(F)[2 + h];
     }
     const float bf = fl[32 + 32 * nh];
+    v8 k[NT][2];
+    relu_pack_tiles<PREC, NT, CL>(acc, k);
     float zt[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const v8 k0 = relu_pack8<PREC>(acc[t], 0), k1 = relu_pack8<PREC>(acc[t], 1);
-        zt[t] = mfma32<PREC>(f1, k1, mfma32<PREC>(f0, k0, f32x16{}))[0] + bf;
-    }
+    for (int t = 0; t < NT; ++t) zt[t] = mfma32<PREC>(f1, k[t][1], mfma32<PREC>(f0, k[t][0], f32x16{}))[0] + bf;
     if constexpr (NT == 1) return zt[0];
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
     return __uint_as_float(r[0]);
 }
 
-// tmask: the caller's 16-point tiles (bits 0-3); the 32-point tiles cover pairs of them
-template <int PREC>
-__device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                            int nh, float fr, float x, float y, float z, uint32_t tmask) {
+template <int PREC, bool CL>
+__device__ __forceinline__ float mlp16_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                               int nh, float fr, float x, float y, float z, uint32_t tmask) {
     // the bundled networks' depth (7 hidden layers) fully unrolled: no loop-carried
     // accumulator copies between layers
     if (nh == 7) {
-        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7>(lp, fl, in0, nh, fr, x, y, z);
-        return mlp32_lowp_nt<PREC, 1, 7>(lp, fl, in0, nh, fr, x, y, z);
+        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
+        return mlp32_lowp_nt<PREC, 1, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
     }
-    if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 0>(lp, fl, in0, nh, fr, x, y, z);
-    return mlp32_lowp_nt<PREC, 1, 0>(lp, fl, in0, nh, fr, x, y, z);
+    if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 0, CL>(lp, fl, in0, nh, fr, x, y, z);
+    return mlp32_lowp_nt<PREC, 1, 0, CL>(lp, fl, in0, nh, fr, x, y, z);
 }
 
+// tmask: the caller's 16-point tiles (bits 0-3); the 32-point tiles cover pairs of them.
+// cl (wave-uniform): the clamped-ReLU form is valid -- the pack is clamped (M.lp_clamp) and
+// every input of the call is within LP_INPUT_BOUND.
+template <int PREC>
+__device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                            int nh, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
+    if constexpr (PREC == NR_PRECISION_BF16) {
+        if (cl) return mlp16_lowp_cl<PREC, true>(lp, fl, in0, nh, fr, x, y, z, tmask);
+    }
+    return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask);
+}
+
+// cl: see mlp16_lowp (ignored in fp32)
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
-                                       int prec, float fr, float x, float y, float z, uint32_t tmask) {
-    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask);
-    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask);
+                                       int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
+    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
+    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     return mlp16_fp32(s32, M.in0, M.nh, fr, x, y, z, tmask);
+}
+
+// wave-uniform: every lane's inputs are within LP_INPUT_BOUND (NaN is not)
+__device__ __forceinline__ bool inputs_in_bound(float x, float y, float z, float f) {
+    const bool ok = __builtin_fabsf(x) <= LP_INPUT_BOUND && __builtin_fabsf(y) <= LP_INPUT_BOUND &&
+                    __builtin_fabsf(z) <= LP_INPUT_BOUND && __builtin_fabsf(f) <= LP_INPUT_BOUND;
+    return __ballot(!ok) == 0;
 }
 
 __device__ __forceinline__ uint32_t tiles_of(uint64_t m) {
@@ -335,17 +421,30 @@ struct Smem16 {
     float *sfl;       // float side of the low-precision pack
 };
 
-__device__ __forceinline__ Smem16 stage16(const MlpArgs &M, int prec) {
+// Stages the packs a kernel of precision PREC reads into LDS.  A reduced-precision kernel
+// that also evaluates fp32 normals (NEED32: k_trace) reads the fp32 pack from global memory
+// (30 KB, L2-resident) unless NR_LOWP_PK32_LDS: normal passes are ~5% of its MLP work, and
+// without the fp32 pack a workgroup's LDS (16.5 KB pack + stash + frames) lets 3 workgroups
+// share a CU instead of 2.  smem16_bytes() is the matching dynamic-LDS size.
+#ifndef NR_LOWP_PK32_LDS
+#define NR_LOWP_PK32_LDS 0
+#endif
+template <int PREC, bool NEED32>
+__device__ __forceinline__ Smem16 stage16(const MlpArgs &M) {
+    constexpr bool lds32 = PREC == NR_PRECISION_FP32 || (NEED32 && NR_LOWP_PK32_LDS);
     Smem16 S;
-    S.s32 = reinterpret_cast<float *>(nr_smem16);
-    S.slp = reinterpret_cast<uint16_t *>(nr_smem16 + M.pk_bytes);
-    S.sfl = reinterpret_cast<float *>(nr_smem16 + M.pk_bytes + M.lp_bytes);
-    const int4 *src = reinterpret_cast<const int4 *>(M.pk);
-    int4 *dst = reinterpret_cast<int4 *>(S.s32);
-    for (int i = threadIdx.x; i < M.pk_bytes / 16; i += blockDim.x) dst[i] = src[i];
-    if (prec != NR_PRECISION_FP32) {
-        src = reinterpret_cast<const int4 *>(M.lp);
-        dst = reinterpret_cast<int4 *>(S.slp);
+    const int off = lds32 ? M.pk_bytes : 0;
+    S.s32 = lds32 ? reinterpret_cast<float *>(nr_smem16) : const_cast<float *>(M.pk);
+    S.slp = reinterpret_cast<uint16_t *>(nr_smem16 + off);
+    S.sfl = reinterpret_cast<float *>(nr_smem16 + off + M.lp_bytes);
+    if constexpr (lds32) {
+        const int4 *src = reinterpret_cast<const int4 *>(M.pk);
+        int4 *dst = reinterpret_cast<int4 *>(S.s32);
+        for (int i = threadIdx.x; i < M.pk_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    }
+    if constexpr (PREC != NR_PRECISION_FP32) {
+        const int4 *src = reinterpret_cast<const int4 *>(M.lp);
+        int4 *dst = reinterpret_cast<int4 *>(S.slp);
         for (int i = threadIdx.x; i < M.lp_bytes / 16; i += blockDim.x) dst[i] = src[i];
         src = reinterpret_cast<const int4 *>(M.lpf);
         dst = reinterpret_cast<int4 *>(S.sfl);
@@ -353,6 +452,12 @@ __device__ __forceinline__ Smem16 stage16(const MlpArgs &M, int prec) {
     }
     __syncthreads();
     return S;
+}
+
+// host side: the dynamic LDS stage16<prec, need32> uses
+inline int smem16_bytes(const MlpArgs &M, int prec, bool need32) {
+    const bool lds32 = prec == NR_PRECISION_FP32 || (need32 && NR_LOWP_PK32_LDS);
+    return (lds32 ? M.pk_bytes : 0) + (prec != NR_PRECISION_FP32 ? M.lp_bytes + M.lpf_bytes : 0);
 }
 
 }  // namespace nr

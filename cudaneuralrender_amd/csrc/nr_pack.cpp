@@ -7,6 +7,7 @@
 // DESIGN.md §4).
 #include "nr_internal.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -107,12 +108,72 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
     return true;
 }
 
-bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-                  const std::vector<std::vector<float>> &B, int precision, std::vector<uint16_t> &a_ops,
-                  std::vector<float> &fl) {
+// Power-of-two scales for the bf16 clamped-ReLU pack: e[l] such that every ReLU layer l's
+// activation, for network inputs within +-LP_INPUT_BOUND, is at most 2^e[l] / 4.  Interval
+// arithmetic in double over the exact f32 weights; the factor 4 covers the bf16 rounding of
+// weights and activations (relative 2^-9 each per layer, ~3% over 8 layers).  Returns false
+// when a scale or a scaled weight would leave the range where bf16 scaling is exact.
+static bool clamp_scales(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                         const std::vector<std::vector<float>> &B, std::vector<int> &e) {
+    const int nl = (int)dims.size() - 1;
+    std::vector<double> lo(dims[0], -(double)LP_INPUT_BOUND), hi(dims[0], (double)LP_INPUT_BOUND);
+    e.assign(nl - 1, 0);
+    for (int l = 0; l < nl - 1; ++l) {
+        const int in = dims[l], out = dims[l + 1];
+        std::vector<double> nlo(out), nhi(out);
+        double top = 0.0;
+        for (int u = 0; u < out; ++u) {
+            double a = B[l][u], b = B[l][u];
+            for (int i = 0; i < in; ++i) {
+                const double w = K[l][(size_t)i * out + u];
+                a += std::min(w * lo[i], w * hi[i]);
+                b += std::max(w * lo[i], w * hi[i]);
+            }
+            nlo[u] = std::max(a, 0.0);  // ReLU
+            nhi[u] = std::max(b, 0.0);
+            top = std::max(top, nhi[u]);
+        }
+        if (!std::isfinite(top)) return false;
+        e[l] = top > 0.0 ? (int)std::ceil(std::log2(top)) + 2 : 0;
+        if (e[l] < -60 || e[l] > 100) return false;
+        lo = nlo;
+        hi = nhi;
+    }
+    // every scaled nonzero weight and bias must stay a normal bf16 / f32 well inside range
+    for (int l = 0; l < nl; ++l) {
+        const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
+        const int sb = l < nl - 1 ? -e[l] : 0;
+        for (float w : K[l])
+            if (w != 0.0f && (std::fabs(std::ldexp((double)w, sw)) < 0x1p-110 || std::fabs(std::ldexp((double)w, sw)) > 0x1p110))
+                return false;
+        for (float b : B[l])
+            if (b != 0.0f && (std::fabs(std::ldexp((double)b, sb)) < 0x1p-110 || std::fabs(std::ldexp((double)b, sb)) > 0x1p110))
+                return false;
+    }
+    return true;
+}
+
+bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &Kin,
+                  const std::vector<std::vector<float>> &Bin, int precision, std::vector<uint16_t> &a_ops,
+                  std::vector<float> &fl, int *clamp) {
     if (!fused_shape_ok(dims)) return false;
     const int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
     const bool bf = precision == NR_PRECISION_BF16;
+    // bf16: layer l's weights scaled by 2^(e[l-1] - e[l]) and its bias by 2^-e[l] (e[-1] = 0,
+    // e[last] = 0), so activations come out scaled by 2^-e[l] and the last layer's output is
+    // unscaled: power-of-two scaling is exact in bf16 and f32, so the network computes the same
+    // values as unscaled, and activations stay below 1 for the clamped ReLU (nr_mlp16.h)
+    std::vector<int> e;
+    const bool cl = bf && clamp_scales(dims, Kin, Bin, e);
+    if (clamp) *clamp = cl ? 1 : 0;
+    std::vector<std::vector<float>> K(Kin), B(Bin);
+    if (cl)
+        for (int l = 0; l < nl; ++l) {
+            const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
+            const int sb = l < nl - 1 ? -e[l] : 0;
+            for (float &w : K[l]) w = std::ldexp(w, sw);
+            for (float &b : B[l]) b = std::ldexp(b, sb);
+        }
     auto cvt = [&](float v) { return bf ? f2bf16(v) : f2fp16(v); };
     auto back = [&](uint16_t h) { return bf ? bf16f(h) : fp16f(h); };
     auto lo = [&](float v) { return cvt(v - back(cvt(v))); };  // the residual's 16-bit value
@@ -124,16 +185,16 @@ bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<fl
     //                  h = 1 slots {wl x3 . xh, wl3 . frh, 0 x4}
     for (int lane = 0; lane < 64; ++lane) {
         const int m = lane & 31, h = lane >> 5;
-        uint16_t *e = &a_ops[(size_t)lane * 8];
+        uint16_t *el = &a_ops[(size_t)lane * 8];
         for (int c = 0; c < 3; ++c) {
             const float w = K[0][(size_t)c * 32 + m];
-            if (h == 0) e[c] = e[3 + c] = cvt(w);
-            else e[c] = lo(w);
+            if (h == 0) el[c] = el[3 + c] = cvt(w);
+            else el[c] = lo(w);
         }
         if (in0 == 4) {
             const float w = K[0][(size_t)3 * 32 + m];
-            if (h == 0) e[6] = e[7] = cvt(w);
-            else e[3] = lo(w);
+            if (h == 0) el[6] = el[7] = cvt(w);
+            else el[3] = lo(w);
         }
     }
     for (int h = 0; h < 2; ++h)
@@ -142,18 +203,18 @@ bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<fl
         const std::vector<float> &Kj = K[j + 1];
         for (int s = 0; s < 2; ++s)
             for (int lane = 0; lane < 64; ++lane)
-                for (int e = 0; e < 8; ++e) {
+                for (int k = 0; k < 8; ++k) {
                     const int m = lane & 31, h = lane >> 5;
-                    a_ops[(size_t)LP32_HID + (size_t)j * LP32_HSTRIDE + (size_t)s * 512 + lane * 8 + e] =
-                        cvt(Kj[(size_t)kin(s, h, e) * 32 + m]);
+                    a_ops[(size_t)LP32_HID + (size_t)j * LP32_HSTRIDE + (size_t)s * 512 + lane * 8 + k] =
+                        cvt(Kj[(size_t)kin(s, h, k) * 32 + m]);
                 }
         for (int h = 0; h < 2; ++h)
             for (int i = 0; i < 16; ++i) fl[32 + 32 * j + h * 16 + i] = B[j + 1][crow(h, i)];
     }
     for (int s = 0; s < 2; ++s)
         for (int h = 0; h < 2; ++h)
-            for (int e = 0; e < 8; ++e)
-                a_ops[(size_t)lp32_final(nh) + (s * 2 + h) * 8 + e] = cvt(K[nl - 1][kin(s, h, e)]);
+            for (int k = 0; k < 8; ++k)
+                a_ops[(size_t)lp32_final(nh) + (s * 2 + h) * 8 + k] = cvt(K[nl - 1][kin(s, h, k)]);
     fl[32 + 32 * nh] = B[nl - 1][0];
     return true;
 }

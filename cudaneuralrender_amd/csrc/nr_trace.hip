@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         for (int i = threadIdx.x; i < nw; i += blockDim.x)
             reinterpret_cast<uint32_t *>(sf)[i] = reinterpret_cast<const uint32_t *>(T.frames)[i];
     }
-    Smem16 S = stage16(M, prec);  // (its __syncthreads also covers sf)
+    Smem16 S = stage16<PREC, true>(M);  // (its __syncthreads also covers sf)
     __shared__ float4 stash[4][STASH][2];  // per wave: {p.xyz, pixel}, {d.xyz, -}
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
         if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
-        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask);
+        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
 // hides behind its MFMAs instead of stalling every wave once per chunk.
 template <int PREC>
 __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
-    Smem16 S = stage16(M, PREC);
+    Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const long stride = (((long)gridDim.x * blockDim.x) >> 6) * 64;
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__rest
         load(base + stride + lane, nx, ny, nz, nf);
         const long rem = n - base;
         const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
-        const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask);
+        const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask, M.lp_clamp && inputs_in_bound(x, y, z, f));
         if (i < n) Y[i] = v;
     }
 }
@@ -501,7 +501,7 @@ hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int
 }
 
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
-    const int sm = smem_bytes(M, prec);
+    const int sm = smem16_bytes(M, prec, false);
     if (prec == NR_PRECISION_BF16)
         hipLaunchKernelGGL(k_mlp16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
     else if (prec == NR_PRECISION_FP16)
@@ -512,7 +512,7 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
 }
 
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {
-    const int sm = smem_bytes(M, prec);
+    const int sm = smem16_bytes(M, prec, true);
     if (T.probe) {
         if (prec == NR_PRECISION_BF16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, true>), dim3(grid), dim3(256), sm, st, A, M, T);

@@ -196,7 +196,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
  * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
  * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
- * the captured hipGraph (for profilers that do not follow graph launches). */
+ * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = bf16 ReLU
+ * by v_pk_max_i16 instead of the conversion's clamp bit (the same pack and values: parity
+ * and A/B of the two forms). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are
@@ -249,6 +251,28 @@ int nr_camera(float rx_deg, float ry_deg, float zoom, float tx, float ty,
 int nr_h5_read_keras(const char *path, int max_layers, int *nlayers, int *dims,
                      float *params /* per layer: kernel (in x out) then bias, or NULL */,
                      size_t params_cap);
+/* HDF5 object tree: the calls HighFive makes for NeuralNetwork::load (neuralNetwork.cpp:86-129)
+ * and simpleInfer's loadModelFromH5 (simpleInfer.cpp:13-79) -- File(fp, ReadOnly),
+ * listObjectNames, getObjectType, getGroup, getNumberObjects, getDataSet, getDimensions,
+ * read -- over the same minimal reader; the headers in include/highfive/ wrap them in HighFive's
+ * class names.  Objects are identified by their object-header addresses; group members
+ * come in HDF5 name order (what HighFive's listObjectNames returns). */
+typedef struct nr_h5_file nr_h5_file;
+#define NR_H5_OTHER 0
+#define NR_H5_GROUP 1
+#define NR_H5_DATASET 2
+int nr_h5_open(const char *path, nr_h5_file **out);
+void nr_h5_close(nr_h5_file *f);
+int nr_h5_root(const nr_h5_file *f, uint64_t *obj);
+int nr_h5_object_type(nr_h5_file *f, uint64_t obj, int *type);
+int nr_h5_num_members(nr_h5_file *f, uint64_t group, size_t *n);
+/* member i of a group: name (NUL-terminated, cap bytes; NULL to query *name_len) and id */
+int nr_h5_member(nr_h5_file *f, uint64_t group, size_t i, char *name, size_t cap, size_t *name_len,
+                 uint64_t *obj);
+/* dims may be NULL to query *ndims */
+int nr_h5_dims(nr_h5_file *f, uint64_t dataset, uint64_t *dims, int cap, int *ndims);
+/* all elements, row-major, converted to float; count must equal the element count */
+int nr_h5_read_f32(nr_h5_file *f, uint64_t dataset, float *out, size_t count);
 /* PNG decode to packed RGBA (image.cu:36-65 packing).  *rgba is malloc'ed; free
  * with nr_free(). */
 int nr_png_load(const char *path, uint32_t **rgba, int *w, int *h);

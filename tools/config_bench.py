@@ -30,6 +30,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--batch", type=int, default=8, help="frames per nr_render_batch launch (0: skip)")
 ap.add_argument("--only", default="", help="comma-separated config names to run (default all)")
+ap.add_argument("--bpc", type=int, default=0, help="nr_set_occupancy (0: the library's default)")
+ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (A/B of the bf16 ReLU forms: 512)")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 
@@ -50,6 +52,8 @@ def run(name, geom, size, prec, steps, shard=None):
         return
     r = nr.Renderer(0).load_h5(nr.geometry_path(geom)).set_precision(prec)
     r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
+    r.set_debug(a.debug)
+    r.set_occupancy(a.bpc)
     band, nsh = (8, 8) if shard is not None else (8, 1)
     rows = nr.shard_rows(size, band, nsh, shard or 0)
     out = torch.zeros(max(a.batch, 1), rows * size, dtype=torch.int32, device="cuda")

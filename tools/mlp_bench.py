@@ -22,14 +22,16 @@ ap.add_argument("--n", type=int, default=1 << 22)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--precision", default="all")
 ap.add_argument("--bpc", default="4")
+ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (A/B of the bf16 ReLU forms: 512)")
 a = ap.parse_args()
 X = np.random.default_rng(0).uniform(-1, 1, size=(a.n, 3)).astype(np.float32)
 dX = torch.from_numpy(X).cuda()
 dY = torch.zeros(a.n, dtype=torch.float32, device="cuda")
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
+r.set_debug(a.debug)
 res = []
-for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else [a.precision]):
+for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else a.precision.split(",")):
     for bpc in (int(b) for b in a.bpc.split(",")):
         r.set_occupancy(bpc)
         r.set_precision(prec)
@@ -44,6 +46,6 @@ for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else [a.precision]
         ms = e0.elapsed_time(e1) / a.iters
         tf = a.n * 14592 / (ms * 1e-3) / 1e12
         util = a.n * 14336 / (ms * 1e-3) / 1e12 / PEAK[prec]
-        res.append({"precision": prec, "tile": "16" if prec == "fp32" else "32", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
+        res.append({"precision": prec, "debug": a.debug, "tile": "16" if prec == "fp32" else "32", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
                     "hidden_layer_mfma_util": round(util, 4), "Gpoints_per_s": round(a.n / ms / 1e6, 2)})
         print(json.dumps(res[-1]), flush=True)
