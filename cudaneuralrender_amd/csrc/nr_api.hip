@@ -1132,7 +1132,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         dX = hx;
     }
     if (c->fused) {
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 4;
+        // workgroups per CU: 4 for fp32; 6 for bf16/fp16, whose 122-VGPR waves (4 per SIMD)
+        // finish a 2^24-point batch 6% sooner with the extra queued workgroups
+        // (profiles/r2_mlp_lowp_dot2_prefetch.txt)
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (c->precision == NR_PRECISION_FP32 ? 4 : 6);
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));

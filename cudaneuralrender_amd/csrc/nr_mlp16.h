@@ -193,10 +193,21 @@ __device__ __forceinline__ f32x16 mfma32(const typename Lowp<PREC>::v8 &a, const
     else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// a.lo * b.lo + a.hi * b.hi + c on packed 16-bit pairs (v_dot2c_f32_{bf16,f16})
 template <int PREC>
-__device__ __forceinline__ uint32_t pk16(typename Lowp<PREC>::e lo, typename Lowp<PREC>::e hi) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    if constexpr (PREC == NR_PRECISION_BF16)
+        return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, a), __builtin_bit_cast(bf16x2, b), c, false);
+    else
+        return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c, false);
 }
+
+// The reduced-precision final layer on the VALU (v_dot2c) instead of 4 MFMAs per 64 points
+#ifndef NR_LOWP_FINAL_DOT2
+#define NR_LOWP_FINAL_DOT2 1
+#endif
 
 // registers 8s..8s+7 of an accumulator -> ReLU'd 16-bit B operand of k-step s:
 // v_cvt_pk rounds pairs (RNE), v_pk_max_i16 against 0 is the ReLU on the 16-bit patterns
@@ -293,19 +304,85 @@ __device__ __forceinline__ void relu_pack_tiles(const f32x16 (&acc)[NT], typenam
     }
 }
 
-// one hidden layer on NT tiles: acc <- W relu(acc) + b
-template <int PREC, int NT, bool CL>
-__device__ __forceinline__ void hidden32(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int jl,
-                                         f32x16 (&acc)[NT]) {
+// One hidden layer's operands: the two K = 16 A operands and the bias (accumulator init).
+#ifndef NR_LOWP_PREFETCH
+#define NR_LOWP_PREFETCH 0
+#endif
+template <int PREC> struct Hidden32W {
+    typename Lowp<PREC>::v8 a0, a1;
+    f32x16 b;
+};
+template <int PREC>
+__device__ __forceinline__ Hidden32W<PREC> hidden32_load(const uint16_t *__restrict__ lp, const float *__restrict__ fl,
+                                                         int jl) {
     typedef typename Lowp<PREC>::v8 v8;
     const int lane = lane_id(), h = lane >> 5;
     const v8 *A = reinterpret_cast<const v8 *>(lp + LP32_HID + jl * LP32_HSTRIDE);
-    const v8 a0 = A[lane], a1 = A[64 + lane];
-    const f32x16 bj = load_bias16(fl + 32 + 32 * jl + 16 * h);
+    return Hidden32W<PREC>{A[lane], A[64 + lane], load_bias16(fl + 32 + 32 * jl + 16 * h)};
+}
+
+// one hidden layer on NT tiles: acc <- W relu(acc) + b
+template <int PREC, int NT, bool CL>
+__device__ __forceinline__ void hidden32(const Hidden32W<PREC> &w, f32x16 (&acc)[NT]) {
+    typedef typename Lowp<PREC>::v8 v8;
     v8 k[NT][2];
     relu_pack_tiles<PREC, NT, CL>(acc, k);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = mfma32<PREC>(a1, k[t][1], mfma32<PREC>(a0, k[t][0], bj));
+    for (int t = 0; t < NT; ++t) acc[t] = mfma32<PREC>(w.a1, k[t][1], mfma32<PREC>(w.a0, k[t][0], w.b));
+}
+
+// The hidden layers.  With NR_LOWP_PREFETCH the next layer's operands are read from LDS
+// before this layer's conversions (24 VGPRs), so their latency hides under the conversions
+// instead of stalling the layer's first MFMA.
+template <int PREC, int NT, int NH, bool CL>
+__device__ __forceinline__ void hidden_layers(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int nh,
+                                              f32x16 (&acc)[NT]) {
+    if constexpr (NR_LOWP_PREFETCH) {
+        if (nh <= 0) return;
+        Hidden32W<PREC> cur = hidden32_load<PREC>(lp, fl, 0);
+        if constexpr (NH > 0) {
+#pragma unroll
+            for (int jl = 0; jl < NH; ++jl) {
+                Hidden32W<PREC> nxt = cur;
+                if (jl + 1 < NH) nxt = hidden32_load<PREC>(lp, fl, jl + 1);
+                hidden32<PREC, NT, CL>(cur, acc);
+                cur = nxt;
+            }
+        } else {
+            for (int jl = 0; jl < nh; ++jl) {
+                const Hidden32W<PREC> nxt = hidden32_load<PREC>(lp, fl, jl + 1 < nh ? jl + 1 : jl);
+                hidden32<PREC, NT, CL>(cur, acc);
+                cur = nxt;
+            }
+        }
+    } else {
+        if constexpr (NH > 0) {
+#pragma unroll
+            for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
+        } else {
+            for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
+        }
+    }
+}
+
+// two floats -> packed 16-bit pair (a in bits 0-15), RNE: one v_cvt_pk
+template <int PREC>
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+    typedef typename Lowp<PREC>::e e16;
+    typedef e16 e16x2 __attribute__((ext_vector_type(2)));
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, e16x2));
+}
+// the value of a packed pair's low / high element
+template <int PREC>
+__device__ __forceinline__ float lo16f(uint32_t p) {
+    if constexpr (PREC == NR_PRECISION_BF16) return __uint_as_float(p << 16);
+    else return (float)__builtin_bit_cast(_Float16, (uint16_t)(p & 0xffffu));
+}
+template <int PREC>
+__device__ __forceinline__ float hi16f(uint32_t p) {
+    if constexpr (PREC == NR_PRECISION_BF16) return __uint_as_float(p & 0xffff0000u);
+    else return (float)__builtin_bit_cast(_Float16, (uint16_t)(p >> 16));
 }
 
 // CL: ReLU by the conversion's clamp (bf16 with the clamped pack, inputs within
@@ -313,7 +390,6 @@ __device__ __forceinline__ void hidden32(const uint16_t *__restrict__ lp, const 
 template <int PREC, int NT, int NH, bool CL>
 __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh_rt, float fr, float x, float y, float z) {
-    typedef typename Lowp<PREC>::e e16;
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
@@ -330,24 +406,57 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
         const f32x16 b0 = load_bias16(fl + 16 * h);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            const e16 xh = (e16)xv[t], yh = (e16)yv[t], zh = (e16)zv[t], fh = (e16)fv[t];
-            const e16 xl = (e16)(xv[t] - (float)xh), yl = (e16)(yv[t] - (float)yh);
-            const e16 zl = (e16)(zv[t] - (float)zh), flo = (e16)(fv[t] - (float)fh);
-            // h = 0: {xh, yh, zh, xl, yl, zl, fh, fl}; h = 1: {xh, yh, zh, fh, 0, 0, 0, 0}
-            // (bit selects, so that nothing is computed under a lane-dependent branch)
-            const uint32_t w0 = pk16<PREC>(xh, yh);
-            const uint32_t w1 = (pk16<PREC>(zh, xl) & ~hm) | (pk16<PREC>(zh, fh) & hm);
-            const uint32_t w2 = pk16<PREC>(yl, zl) & ~hm;
-            const uint32_t w3 = pk16<PREC>(fh, flo) & ~hm;
-            acc[t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){w0, w1, w2, w3}), b0);
+            // B operand, h = 0: {xh, yh | zh, xl | yl, zl | fh, fl}; h = 1: {xh, yh | zh, fh | 0 | 0}
+            // (the residuals x - xh are exact in f32; bit selects, so that nothing is computed
+            // under a lane-dependent branch)
+            const uint32_t p0 = cvt2<PREC>(xv[t], yv[t]);                             // xh, yh
+            const float dx = xv[t] - lo16f<PREC>(p0), dy = yv[t] - hi16f<PREC>(p0);
+            const uint32_t q = cvt2<PREC>(zv[t], dx);                                  // zh, xl
+            const uint32_t r = cvt2<PREC>(dy, zv[t] - lo16f<PREC>(q));                 // yl, zl
+            uint32_t f = 0;                                                            // fh, fl
+            if (in0 == 4) {
+                const uint32_t f0 = cvt2<PREC>(fv[t], 0.0f);
+                f = cvt2<PREC>(fv[t], fv[t] - lo16f<PREC>(f0));
+            }
+            const uint32_t w1 = (q & ~hm) | (((q & 0xffffu) | (f << 16)) & hm);
+            acc[t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){p0, w1, r & ~hm, f & ~hm}), b0);
         }
     }
-    if constexpr (NH > 0) {
+    hidden_layers<PREC, NT, NH, CL>(lp, fl, nh, acc);
+#if NR_LOWP_FINAL_DOT2
+    // final 32 -> 1 layer on the VALU: lane l holds 16 of point (l & 31)'s units as the 8
+    // packed pairs of its B operands, and the pack's row-0 A operand of (k-step s, half h)
+    // holds their weights in the same order, so 8 v_dot2c_f32_{bf16,f16} per tile give the
+    // half's partial sum (k-step 0 then 1, pairs ascending); one v_permlane32_swap brings
+    // the other half's partial (and tile 1 to lanes 32-63), then half 0 + half 1 + bias.
+    // Four 32x32x16 MFMAs (1 useful row of 32) per 64 points otherwise.
+    const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(nh));
+    const u32x4 wf[2] = {F4[h], F4[2 + h]};
+    const float bf = fl[32 + 32 * nh];
+    v8 k[NT][2];
+    relu_pack_tiles<PREC, NT, CL>(acc, k);
+    float zt[NT];
 #pragma unroll
-        for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT, CL>(lp, fl, jl, acc);
-    } else {
-        for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT, CL>(lp, fl, jl, acc);
+    for (int t = 0; t < NT; ++t) {
+        float a = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const u32x4 kv = __builtin_bit_cast(u32x4, k[t][st]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a = dot2<PREC>(kv[q], wf[st][q], a);
+        }
+        zt[t] = a;
     }
+    float z0, z1;
+    if constexpr (NT == 1) {
+        half_views(zt[0], z0, z1);
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
+        z0 = __uint_as_float(r[0]);
+        z1 = __uint_as_float(r[1]);
+    }
+    return (z0 + z1) + bf;
+#else
     // final layer: row 0 of A (lanes 0 and 32) holds the weights, every other row is 0;
     // the accumulator starts at 0 and the bias is added to register 0 alone
     const uint16_t *F = lp + lp32_final(nh);
@@ -365,6 +474,7 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
     if constexpr (NT == 1) return zt[0];
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
     return __uint_as_float(r[0]);
+#endif
 }
 
 template <int PREC, bool CL>

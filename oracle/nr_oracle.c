@@ -127,8 +127,105 @@ static float round_fp16(float x)
     return x < 0 ? -r : r;
 }
 
-static void mlp_point(const or_mlp *m, const float *x, float *y, float *buf0, float *buf1, int precision)
+/* The reduced-precision MLP as libnr computes it on the GPU (nr_mlp16.h mlp32_lowp_nt, the pack
+ * of nr_pack.cpp pack_lowp_32), for the networks the fused kernels take ([3|4, 32 x k, 1]):
+ *   layer 0   one 32x32x16 MFMA over the hi/lo split of weights and inputs
+ *             (w x ~ wh xh + wh xl + wl xh, every 16-bit part RNE; the residual x - xh in f32),
+ *             accumulator initialised with the bias;
+ *   hidden    activations relu(z) rounded to 16 bits (RNE), two K = 16 MFMAs: units 0-15
+ *             onto the bias, then units 16-31;
+ *   final     per lane half (units {16s + 8(e >> 2) + 4h + (e & 3)}), eight v_dot2c steps
+ *             (pairs e = 0-1, 2-3, ... of k-step 0, then of k-step 1), then
+ *             (half 0 + half 1) + bias in f32.
+ * An MFMA or dot2 step is modelled as the exact sum of its products and its accumulator,
+ * rounded once to f32 (the products of 16-bit operands are exact; the hardware's internal
+ * summation order is not documented), so this is an emulation for tolerance contracts, not a
+ * bit-exact restatement.  The clamped-ReLU pack's power-of-two scaling changes no value. */
+static float r16(float x, int prec) { return prec == 1 ? round_bf16(x) : round_fp16(x); }
+
+static int fused_shape(const or_mlp *m)
 {
+    int nl = m->nlayers;
+    if (nl < 2 || (m->dims[0] != 3 && m->dims[0] != 4) || m->dims[nl] != 1) return 0;
+    for (int l = 1; l < nl; ++l) if (m->dims[l] != 32) return 0;
+    return 1;
+}
+
+/* the 16-bit weights of a fused network, rounded once (layer 0: hi and lo parts) */
+typedef struct {
+    int prec;
+    float w0h[32 * 4], w0l[32 * 4];
+    float *wr;             /* hidden layers then the final layer, out-major like or_mlp */
+} or_lowp;
+
+static int lowp_init(or_lowp *q, const or_mlp *m, int prec)
+{
+    const int in0 = m->dims[0], nl = m->nlayers;
+    q->prec = prec;
+    for (int i = 0; i < 32 * in0; ++i) {
+        float w = m->W[0][i];
+        q->w0h[i] = r16(w, prec);
+        q->w0l[i] = r16(w - q->w0h[i], prec);
+    }
+    q->wr = (float *)malloc(sizeof(float) * (size_t)(32 * 32 * (nl - 2) + 32));
+    if (!q->wr) return -1;
+    float *o = q->wr;
+    for (int l = 1; l < nl; ++l) {
+        int n = 32 * m->dims[l + 1];
+        for (int i = 0; i < n; ++i) o[i] = r16(m->W[l][i], prec);
+        o += n;
+    }
+    return 0;
+}
+
+static void mlp_point_gpu_lowp(const or_mlp *m, const or_lowp *q, const float *x, float *y)
+{
+    const int in0 = m->dims[0], nl = m->nlayers, prec = q->prec;
+    float xh[4], xl[4], a[32], z[32];
+    for (int c = 0; c < in0; ++c) {
+        xh[c] = r16(x[c], prec);
+        xl[c] = r16(x[c] - xh[c], prec);
+    }
+    for (int u = 0; u < 32; ++u) {               /* layer 0 */
+        const float *wh = q->w0h + (size_t)u * in0, *wl = q->w0l + (size_t)u * in0;
+        double sum = m->b[0][u];
+        for (int c = 0; c < in0; ++c)
+            sum += (double)wh[c] * xh[c] + (double)wh[c] * xl[c] + (double)wl[c] * xh[c];
+        z[u] = (float)sum;
+    }
+    const float *wl = q->wr;
+    for (int l = 1; l < nl - 1; ++l, wl += 32 * 32) {   /* hidden 32 x 32 */
+        for (int k = 0; k < 32; ++k) a[k] = r16(fmaxf(z[k], 0.0f), prec);
+        for (int u = 0; u < 32; ++u) {
+            const float *w = wl + (size_t)u * 32;
+            double s0 = m->b[l][u];
+            for (int k = 0; k < 16; ++k) s0 += (double)w[k] * a[k];
+            double s1 = (float)s0;
+            for (int k = 16; k < 32; ++k) s1 += (double)w[k] * a[k];
+            z[u] = (float)s1;
+        }
+    }
+    for (int k = 0; k < 32; ++k) a[k] = r16(fmaxf(z[k], 0.0f), prec);
+    float half[2];
+    for (int h = 0; h < 2; ++h) {                /* final: v_dot2c chain per lane half */
+        float acc = 0.0f;
+        for (int s = 0; s < 2; ++s)
+            for (int e = 0; e < 8; e += 2) {
+                int k0 = 16 * s + 8 * (e >> 2) + 4 * h + (e & 3), k1 = k0 + 1;
+                acc = (float)((double)acc + (double)wl[k0] * a[k0] + (double)wl[k1] * a[k1]);
+            }
+        half[h] = acc;
+    }
+    y[0] = (half[0] + half[1]) + m->b[nl - 1][0];
+}
+
+static void mlp_point(const or_mlp *m, const or_lowp *q, const float *x, float *y, float *buf0, float *buf1,
+                      int precision)
+{
+    if (precision != 0 && q) {
+        mlp_point_gpu_lowp(m, q, x, y);
+        return;
+    }
     const float *a = x;
     float *z = buf0;
     for (int l = 0; l < m->nlayers; ++l) {
@@ -156,6 +253,29 @@ static void mlp_point(const or_mlp *m, const float *x, float *y, float *buf0, fl
     }
 }
 
+/* Per-point precision (render: marching points in the render's precision, normal points in
+ * fp32 as on the GPU). */
+static void mlp_forward_mixed(const or_mlp *m, const or_lowp *q, const float *X, long n, int in_stride, float *Y,
+                              const unsigned char *prec, int nthreads)
+{
+    int out = m->dims[m->nlayers];
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        float *b0 = (float *)malloc(sizeof(float) * (size_t)m->maxw);
+        float *b1 = (float *)malloc(sizeof(float) * (size_t)m->maxw);
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+        for (long i = 0; i < n; ++i)
+            mlp_point(m, q, X + (size_t)i * in_stride, Y + (size_t)i * out, b0, b1, prec[i]);
+        free(b0); free(b1);
+    }
+    (void)nthreads;
+}
+
 /* Batched forward: X is [n][in_stride] with the first dims[0] columns used, Y is
  * [n][dims[nlayers]].  Mirrors NeuralNetwork::forward(batch) (neuralNetwork.cpp:54). */
 int or_mlp_forward(int nlayers, const int *dims, const float *params,
@@ -166,6 +286,11 @@ int or_mlp_forward(int nlayers, const int *dims, const float *params,
     if (or_mlp_init(&m, nlayers, dims, params)) return -1;
     if (in_stride < dims[0]) return -2;
     int out = dims[nlayers];
+    or_lowp q, *qp = NULL;
+    if (precision != 0 && fused_shape(&m)) {
+        if (lowp_init(&q, &m, precision)) return -3;
+        qp = &q;
+    }
 #ifdef _OPENMP
     if (nthreads <= 0) nthreads = omp_get_max_threads();
 #pragma omp parallel num_threads(nthreads)
@@ -177,10 +302,11 @@ int or_mlp_forward(int nlayers, const int *dims, const float *params,
 #pragma omp for schedule(static)
 #endif
         for (long i = 0; i < n; ++i)
-            mlp_point(&m, X + (size_t)i * in_stride, Y + (size_t)i * out, b0, b1, precision);
+            mlp_point(&m, qp, X + (size_t)i * in_stride, Y + (size_t)i * out, b0, b1, precision);
         free(b0); free(b1);
     }
     (void)nthreads;
+    if (qp) free(q.wr);
     return 0;
 }
 
@@ -465,6 +591,17 @@ static int intersectSphere(f3 o, f3 d, float r, float *tnear, float *tfar) /* :1
 /* stats[0] = ray-steps (MLP evaluations of stepping rays), stats[1] = shade
  * evaluations (4 per coloured ray), stats[2] = host iterations executed,
  * stats[3] = rays that hit the bounding sphere, stats[4] = coloured pixels. */
+/* or_render_ex: `precision` 1/2 marches with the GPU's bf16/fp16 MLP arithmetic
+ * (mlp_point_gpu_lowp; normals stay fp32, as on the GPU), and only rows [y0, y1) of the
+ * W x H frame are rendered into out ((y1 - y0) x W) -- a crop of the full frame with the
+ * full frame's rays. */
+int or_render_ex(int nlayers, const int *dims, const float *params,
+                 const float *inv_view, const float *normal, int frame,
+                 int color_type, int num_inputs, int scene,
+                 const uint32_t *matcap, int mw, int mh,
+                 int W, int H, int max_steps, uint32_t *out, long long *stats,
+                 int nthreads, int precision, int y0, int y1);
+
 int or_render(int nlayers, const int *dims, const float *params,
               const float *inv_view, const float *normal, int frame,
               int color_type, int num_inputs, int scene,
@@ -472,15 +609,33 @@ int or_render(int nlayers, const int *dims, const float *params,
               int W, int H, int max_steps, uint32_t *out, long long *stats,
               int nthreads)
 {
+    return or_render_ex(nlayers, dims, params, inv_view, normal, frame, color_type, num_inputs, scene,
+                        matcap, mw, mh, W, H, max_steps, out, stats, nthreads, 0, 0, H);
+}
+
+int or_render_ex(int nlayers, const int *dims, const float *params,
+                 const float *inv_view, const float *normal, int frame,
+                 int color_type, int num_inputs, int scene,
+                 const uint32_t *matcap, int mw, int mh,
+                 int W, int H, int max_steps, uint32_t *out, long long *stats,
+                 int nthreads, int precision, int y0, int y1)
+{
     or_mlp m;
     if (or_mlp_init(&m, nlayers, dims, params)) return -1;
     if (num_inputs != 3 && num_inputs != 4) return -2;
     if (dims[0] != num_inputs || dims[nlayers] != 1) return -3;
     if (color_type == 1 && (!matcap || mw < 1 || mh < 1)) return -4;
+    if (y0 < 0 || y1 > H || y0 > y1) return -6;
+    if (precision != 0 && !fused_shape(&m)) return -7;
     or_settings S = { inv_view, normal, frame, color_type, num_inputs, scene, matcap, mw, mh };
-    long npix = (long)W * H;
+    long npix = (long)W * (y1 - y0);
     long long st[5] = { 0, 0, 0, 0, 0 };
     if (npix <= 0) { if (stats) memcpy(stats, st, sizeof st); return 0; }
+    or_lowp q, *qp = NULL;
+    if (precision != 0) {
+        if (lowp_init(&q, &m, precision)) return -5;
+        qp = &q;
+    }
 
     unsigned *mask = (unsigned *)calloc(npix, sizeof(unsigned));
     unsigned *idmap = (unsigned *)calloc(npix, sizeof(unsigned));
@@ -489,8 +644,10 @@ int or_render(int nlayers, const int *dims, const float *params,
     float *far_ = (float *)calloc(npix, sizeof(float));
     float *batch = (float *)calloc((size_t)npix * num_inputs * COLOR_MASK_VAL, sizeof(float));
     float *sdf = (float *)calloc((size_t)npix * COLOR_MASK_VAL, sizeof(float));
-    if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf) {
-        free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf);
+    unsigned char *bprec = (unsigned char *)calloc((size_t)npix * COLOR_MASK_VAL, 1);
+    if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf || !bprec) {
+        free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf); free(bprec);
+        if (qp) free(q.wr);
         return -5;
     }
     for (long i = 0; i < npix; ++i) out[i] = 0;   /* caller's cudaMemset (main.cpp:408) */
@@ -499,9 +656,9 @@ int or_render(int nlayers, const int *dims, const float *params,
     f3 origin = mk3(dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 0),
                     dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 4),
                     dot4((const float[4]){ 0, 0, 0, 1 }, inv_view + 8));
-    for (int y = 0; y < H; ++y)
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < W; ++x) {
-            long id = (long)y * W + x;
+            long id = (long)(y - y0) * W + x;
             float u = ((float)x / (float)W) * 2.0f - 1.0f;
             float v = ((float)y / (float)H) * 2.0f - 1.0f;
             f3 d = normalize3(mk3(u, v, -2.0f));
@@ -539,9 +696,11 @@ int or_render(int nlayers, const int *dims, const float *params,
             if (mv == 1) {
                 batch[bi] = points[3 * i]; batch[bi + 1] = points[3 * i + 1]; batch[bi + 2] = points[3 * i + 2];
                 if (ni == 4) batch[bi + 3] = (float)frame;
+                bprec[idmap[i]] = (unsigned char)precision;
             } else {
                 for (unsigned q = 0; q < mv; ++q) {
                     size_t o = bi + (size_t)q * ni;
+                    bprec[idmap[i] + q] = 0;
                     batch[o] = points[3 * i] + TET[3 * q] * NORMAL_EPSILON;
                     batch[o + 1] = points[3 * i + 1] + TET[3 * q + 1] * NORMAL_EPSILON;
                     batch[o + 2] = points[3 * i + 2] + TET[3 * q + 2] * NORMAL_EPSILON;
@@ -552,7 +711,7 @@ int or_render(int nlayers, const int *dims, const float *params,
         st[0] += nstep; st[1] += 4 * nshade; st[2]++;
         long long shaded = 0;
         /* nn.forward(batch) :661 */
-        or_mlp_forward(nlayers, dims, params, batch, batchSize, ni, sdf, 0, nthreads);
+        mlp_forward_mixed(&m, qp, batch, batchSize, ni, sdf, bprec, nthreads);
         /* singleMarch :416-477 */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : omp_get_max_threads()) reduction(+:shaded)
@@ -589,7 +748,8 @@ int or_render(int nlayers, const int *dims, const float *params,
         st[4] += shaded;
     }
     if (stats) memcpy(stats, st, sizeof st);
-    free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf);
+    free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf); free(bprec);
+    if (qp) free(q.wr);
     return 0;
 }
 

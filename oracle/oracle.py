@@ -11,7 +11,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO = os.path.join(HERE, "_build", "liboracle.so")
+# OR_LIBRARY: another build of the same source (tools/contract_drift.py: -ffp-contract=fast)
+SO = os.environ.get("OR_LIBRARY") or os.path.join(HERE, "_build", "liboracle.so")
 
 _lib = None
 
@@ -32,6 +33,8 @@ def lib():
         L.or_mlp_forward.argtypes = [I, P, P, P, ctypes.c_long, I, P, I, I]
         L.or_render.restype = I
         L.or_render.argtypes = [I, P, P, P, P, I, I, I, I, P, I, I, I, I, I, P, P, I]
+        L.or_render_ex.restype = I
+        L.or_render_ex.argtypes = [I, P, P, P, P, I, I, I, I, P, I, I, I, I, I, P, P, I, I, I, I]
         L.or_scene_sdf.restype = ctypes.c_float
         L.or_scene_sdf.argtypes = [ctypes.c_float] * 4 + [I, I]
         L.nr_tanh_f.restype = ctypes.c_float
@@ -80,8 +83,11 @@ class OracleNet:
         return Y
 
     def render(self, W, H, inv_view, normal, frame=0, color_type=0, num_inputs=3, scene=0, matcap=None,
-               max_steps=6000, nthreads=0):
-        out = np.zeros((H, W), np.uint32)
+               max_steps=6000, nthreads=0, precision=0, rows=None):
+        """precision 1/2: the GPU's bf16/fp16 MLP arithmetic (nr_oracle.c mlp_point_gpu_lowp) for
+        the marching points, fp32 normals.  rows=(y0, y1): render only those rows of the frame."""
+        y0, y1 = rows if rows is not None else (0, H)
+        out = np.zeros((y1 - y0, W), np.uint32)
         stats = np.zeros(5, np.int64)
         iv = np.ascontiguousarray(inv_view, np.float32)
         nm = np.ascontiguousarray(normal, np.float32)
@@ -90,9 +96,9 @@ class OracleNet:
             mp, mw, mh = mc.ctypes.data, mc.shape[1], mc.shape[0]
         else:
             mc, mp, mw, mh = None, None, 0, 0
-        rc = lib().or_render(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, iv.ctypes.data,
-                             nm.ctypes.data, frame, color_type, num_inputs, scene, mp, mw, mh, W, H, max_steps,
-                             out.ctypes.data, stats.ctypes.data, nthreads)
+        rc = lib().or_render_ex(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, iv.ctypes.data,
+                                nm.ctypes.data, frame, color_type, num_inputs, scene, mp, mw, mh, W, H, max_steps,
+                                out.ctypes.data, stats.ctypes.data, nthreads, precision, y0, y1)
         assert rc == 0, rc
         keys = ["ray_steps", "shade_evals", "iterations", "rays_hit", "rays_shaded"]
         return out, dict(zip(keys, (int(v) for v in stats)))

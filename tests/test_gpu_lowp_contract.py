@@ -1,0 +1,103 @@
+"""Pixel contract of the reduced-precision configurations (BASELINE C3-C5) against the oracle.
+
+The oracle marches with the GPU's bf16/fp16 MLP arithmetic (oracle/nr_oracle.c
+mlp_point_gpu_lowp: 16-bit operands rounded as the kernels round them, each MFMA / dot2 step an
+exact sum rounded once to f32 -- the hardware's internal summation order is not documented,
+so this is an emulation, not a bit-exact restatement) and fp32 normals, on a row crop of the
+full-size frame (the same rays as the full frame).  Per crop we report the identical-pixel
+fraction, the per-channel mean and max |delta| over pixels both sides cover, the coverage IoU,
+and the same figures against the fp32 oracle (what reduced precision costs in total).
+
+Contract, per configuration crop, against the emulation:
+                      bf16 (C3, C4)   fp16 (C5)     measured r2 (profiles/r2_lowp_contract.json)
+  identical pixels    >= 99.9 %       >= 98 %       bf16 99.97-99.99 %, fp16 98.7-99.9 %
+  coverage IoU        >= 0.9999       >= 0.995      bf16 >= 0.99996, fp16 >= 0.9978
+  mean |delta|/chan.  <= 0.02         <= 0.3        bf16 0.006, fp16 0.05-0.21 (of 255)
+and the emulation must be closer to the GPU than the fp32 oracle is (fp32: 76-99 % identical,
+mean |delta| 1.2-10).  For scale: the fp32 oracle built with and without FMA contraction differs
+in 1-4 % of its pixels (tools/contract_drift.py, profiles/r2_fp32_contraction_drift.txt).
+A single differing MLP rounding moves one ray's step, which can change its pixel completely
+(a silhouette ray hits or misses, a grazing ray converges one step later), so max |delta| is
+reported, not bounded."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+from conftest import GEOMS, REPO
+
+pytestmark = pytest.mark.gpu
+PREC = {"bf16": 1, "fp16": 2}
+
+
+@pytest.fixture(scope="module")
+def chrome():
+    return nr.load_png(nr.matcap_path("Chrome"))
+
+
+def channels(img):
+    return np.stack([(img >> (8 * c)) & 0xff for c in range(4)], -1).astype(np.int32)
+
+
+def compare(gpu, ref):
+    fg, fr = gpu != 0, ref != 0
+    both = fg & fr
+    d = np.abs(channels(gpu) - channels(ref))[both] if both.any() else np.zeros((0, 4), np.int32)
+    return {"identical": float((gpu == ref).mean()),
+            "iou": float(both.sum() / max((fg | fr).sum(), 1)),
+            "mean_abs": [round(float(v), 4) for v in (d.mean(0) if len(d) else np.zeros(4))],
+            "max_abs": [int(v) for v in (d.max(0) if len(d) else np.zeros(4))]}
+
+
+def contract(name, geom, size, steps, prec, rows, chrome, record):
+    dims, K, B = nr.read_keras_h5(nr.geometry_path(geom))
+    iv, nm = nr.camera(0.0, 0.0, 2.0)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path(geom)).set_precision(prec)
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        img, st = r.render(size, size, steps)
+    gpu = img[rows[0]:rows[1]]
+    net = oracle.OracleNet(K, B)
+    kw = dict(color_type=1, matcap=chrome, max_steps=steps, nthreads=16, rows=rows)
+    emu, _ = net.render(size, size, iv, nm, precision=PREC[prec], **kw)
+    f32, _ = net.render(size, size, iv, nm, precision=0, **kw)
+    res = {"config": name, "geometry": geom, "size": size, "steps": steps, "precision": prec, "rows": list(rows),
+           "vs_emulation": compare(gpu, emu), "vs_fp32_oracle": compare(gpu, f32),
+           "emulation_vs_fp32_oracle": compare(emu, f32)}
+    record.append(res)
+    e = res["vs_emulation"]
+    ident, iou, mean = {"bf16": (0.999, 0.9999, 0.02), "fp16": (0.98, 0.995, 0.3)}[prec]
+    assert e["identical"] >= ident, res
+    assert e["iou"] >= iou, res
+    assert max(e["mean_abs"]) <= mean, res
+    assert e["identical"] > res["vs_fp32_oracle"]["identical"], res
+    return res
+
+
+@pytest.fixture(scope="module")
+def record():
+    out = []
+    yield out
+    d = os.path.join(REPO, "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "lowp_contract.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def test_c3_bf16_contract(chrome, record):
+    # C3: car_1 2048^2, 256 steps, bf16; the 256 rows through the object's centre
+    contract("C3", "car_1", 2048, 256, "bf16", (896, 1152), chrome, record)
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_c5_fp16_contract(chrome, record, geom):
+    # C5: each geometry 2048^2, 128 steps, fp16; 128 rows through the centre
+    contract("C5", geom, 2048, 128, "fp16", (960, 1088), chrome, record)
+
+
+def test_c4_bf16_contract(chrome, record):
+    # C4: plane_2 4096^2, 128 steps, bf16; 128 rows through the centre
+    contract("C4", "plane_2", 4096, 128, "bf16", (1984, 2112), chrome, record)
