@@ -870,7 +870,13 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // 3 workgroups (12 waves) per CU once several frames share the launch: the third
         // wave per SIMD lifts the bulk rate, and the frames' tails overlap instead of
         // adding up (tools/batch_bench.py); a lone frame keeps the single-frame default
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (n >= 4 ? 3 : 2);
+        // and a 4th once a launch holds >= 8 M fp32 pixels (the 38 KB fp32 workgroup fits 4 to a
+        // CU since r2: 1024^2 x 32 frames 1.902 -> 1.866 ms/frame; one 8-way shard x 8 frames,
+        // 1 M pixels, 0.366 -> 0.410, profiles/r2_occupancy.txt).  bf16/fp16 waves need 150
+        // VGPRs: 3 per SIMD at most.
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu
+                        : n < 4 ? 2
+                        : (c->precision == NR_PRECISION_FP32 && npix * n >= ((size_t)8 << 20)) ? 4 : 3;
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         int rc2;

@@ -167,12 +167,13 @@ __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0
 //     bias as the accumulator init;
 //   * hidden layers: two K = 16 MFMAs per tile (K = 32), bias as the accumulator init; the
 //     f32 result is its own next B operand with no lane movement (registers 8s..8s+7 are
-//     k-step s, the pack orders the weights to match): per tile and layer 8
-//     v_cvt_pk + 8 v_pk_max_i16 (the ReLU on the 16-bit patterns) against 2 MFMAs of 32
-//     cycles -- the 16x16x32 form needed as many VALU per point for half the MFMA time
-//     per instruction and held the issue port twice as long per point;
-//   * final 32 -> 1 layer: two MFMAs with the weights in row 0 of A, z in register 0 of
-//     lanes 0-31; one v_permlane32_swap returns tile 1's z to lanes 32-63.
+//     k-step s, the pack orders the weights to match): per tile and layer 8 v_cvt_pk with
+//     the ReLU folded into their clamp bit (bf16, relu_clamp_bf16_x*; otherwise 8 more
+//     v_pk_max_i16) against 2 MFMAs of 32 cycles -- the 16x16x32 form needed as many VALU
+//     per point for half the MFMA time per instruction and held the issue port twice as
+//     long per point;
+//   * final 32 -> 1 layer: 8 v_dot2c per tile over the same packed activations, the two
+//     lane halves' partial sums joined by one v_permlane32_swap.
 // The lane-half views of the inputs come from v_permlane32_swap as well (no ds_bpermute).
 template <int PREC> struct Lowp;
 template <> struct Lowp<NR_PRECISION_BF16> { typedef __bf16 e; typedef bf16x8 v8; };
@@ -203,11 +204,6 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
     else
         return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b), c, false);
 }
-
-// The reduced-precision final layer on the VALU (v_dot2c) instead of 4 MFMAs per 64 points
-#ifndef NR_LOWP_FINAL_DOT2
-#define NR_LOWP_FINAL_DOT2 1
-#endif
 
 // registers 8s..8s+7 of an accumulator -> ReLU'd 16-bit B operand of k-step s:
 // v_cvt_pk rounds pairs (RNE), v_pk_max_i16 against 0 is the ReLU on the 16-bit patterns
@@ -305,9 +301,9 @@ __device__ __forceinline__ void relu_pack_tiles(const f32x16 (&acc)[NT], typenam
 }
 
 // One hidden layer's operands: the two K = 16 A operands and the bias (accumulator init).
-#ifndef NR_LOWP_PREFETCH
-#define NR_LOWP_PREFETCH 0
-#endif
+// (Reading the next layer's operands one layer ahead, to hide their LDS latency under the
+// conversions, measured no faster and made the single-frame bf16 tracer spill:
+// profiles/r2_mlp_lowp_dot2_prefetch.txt.)
 template <int PREC> struct Hidden32W {
     typename Lowp<PREC>::v8 a0, a1;
     f32x16 b;
@@ -331,37 +327,14 @@ __device__ __forceinline__ void hidden32(const Hidden32W<PREC> &w, f32x16 (&acc)
     for (int t = 0; t < NT; ++t) acc[t] = mfma32<PREC>(w.a1, k[t][1], mfma32<PREC>(w.a0, k[t][0], w.b));
 }
 
-// The hidden layers.  With NR_LOWP_PREFETCH the next layer's operands are read from LDS
-// before this layer's conversions (24 VGPRs), so their latency hides under the conversions
-// instead of stalling the layer's first MFMA.
 template <int PREC, int NT, int NH, bool CL>
 __device__ __forceinline__ void hidden_layers(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int nh,
                                               f32x16 (&acc)[NT]) {
-    if constexpr (NR_LOWP_PREFETCH) {
-        if (nh <= 0) return;
-        Hidden32W<PREC> cur = hidden32_load<PREC>(lp, fl, 0);
-        if constexpr (NH > 0) {
+    if constexpr (NH > 0) {
 #pragma unroll
-            for (int jl = 0; jl < NH; ++jl) {
-                Hidden32W<PREC> nxt = cur;
-                if (jl + 1 < NH) nxt = hidden32_load<PREC>(lp, fl, jl + 1);
-                hidden32<PREC, NT, CL>(cur, acc);
-                cur = nxt;
-            }
-        } else {
-            for (int jl = 0; jl < nh; ++jl) {
-                const Hidden32W<PREC> nxt = hidden32_load<PREC>(lp, fl, jl + 1 < nh ? jl + 1 : jl);
-                hidden32<PREC, NT, CL>(cur, acc);
-                cur = nxt;
-            }
-        }
+        for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
     } else {
-        if constexpr (NH > 0) {
-#pragma unroll
-            for (int jl = 0; jl < NH; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
-        } else {
-            for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
-        }
+        for (int jl = 0; jl < nh; ++jl) hidden32<PREC, NT, CL>(hidden32_load<PREC>(lp, fl, jl), acc);
     }
 }
 
@@ -423,13 +396,13 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
         }
     }
     hidden_layers<PREC, NT, NH, CL>(lp, fl, nh, acc);
-#if NR_LOWP_FINAL_DOT2
     // final 32 -> 1 layer on the VALU: lane l holds 16 of point (l & 31)'s units as the 8
     // packed pairs of its B operands, and the pack's row-0 A operand of (k-step s, half h)
     // holds their weights in the same order, so 8 v_dot2c_f32_{bf16,f16} per tile give the
     // half's partial sum (k-step 0 then 1, pairs ascending); one v_permlane32_swap brings
     // the other half's partial (and tile 1 to lanes 32-63), then half 0 + half 1 + bias.
-    // Four 32x32x16 MFMAs (1 useful row of 32) per 64 points otherwise.
+    // (Four 32x32x16 MFMAs, 1 useful row of 32, per 64 points before: profiles/
+    // r2_mlp_lowp_dot2_prefetch.txt.)
     const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(nh));
     const u32x4 wf[2] = {F4[h], F4[2 + h]};
     const float bf = fl[32 + 32 * nh];
@@ -456,25 +429,6 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
         z1 = __uint_as_float(r[1]);
     }
     return (z0 + z1) + bf;
-#else
-    // final layer: row 0 of A (lanes 0 and 32) holds the weights, every other row is 0;
-    // the accumulator starts at 0 and the bias is added to register 0 alone
-    const uint16_t *F = lp + lp32_final(nh);
-    v8 f0 = {}, f1 = {};
-    if ((lane & 31) == 0) {
-        f0 = reinterpret_cast<const v8 *>(F)[h];
-        f1 = reinterpret_cast<const v8 *>(F)[2 + h];
-    }
-    const float bf = fl[32 + 32 * nh];
-    v8 k[NT][2];
-    relu_pack_tiles<PREC, NT, CL>(acc, k);
-    float zt[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) zt[t] = mfma32<PREC>(f1, k[t][1], mfma32<PREC>(f0, k[t][0], f32x16{}))[0] + bf;
-    if constexpr (NT == 1) return zt[0];
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
-    return __uint_as_float(r[0]);
-#endif
 }
 
 template <int PREC, bool CL>
@@ -533,15 +487,13 @@ struct Smem16 {
 
 // Stages the packs a kernel of precision PREC reads into LDS.  A reduced-precision kernel
 // that also evaluates fp32 normals (NEED32: k_trace) reads the fp32 pack from global memory
-// (30 KB, L2-resident) unless NR_LOWP_PK32_LDS: normal passes are ~5% of its MLP work, and
-// without the fp32 pack a workgroup's LDS (16.5 KB pack + stash + frames) lets 3 workgroups
-// share a CU instead of 2.  smem16_bytes() is the matching dynamic-LDS size.
-#ifndef NR_LOWP_PK32_LDS
-#define NR_LOWP_PK32_LDS 0
-#endif
+// (30 KB, L2-resident): normal passes are ~5% of its MLP work, and without the fp32 pack a
+// workgroup's LDS (16.5 KB pack + stash + frames) lets 3 workgroups share a CU instead of 2
+// (bf16 C3 batch 2.09 -> 1.81 ms/frame, profiles/r2_lowp_clamp_lds_ab.txt).
+// smem16_bytes() is the matching dynamic-LDS size.
 template <int PREC, bool NEED32>
 __device__ __forceinline__ Smem16 stage16(const MlpArgs &M) {
-    constexpr bool lds32 = PREC == NR_PRECISION_FP32 || (NEED32 && NR_LOWP_PK32_LDS);
+    constexpr bool lds32 = PREC == NR_PRECISION_FP32;
     Smem16 S;
     const int off = lds32 ? M.pk_bytes : 0;
     S.s32 = lds32 ? reinterpret_cast<float *>(nr_smem16) : const_cast<float *>(M.pk);
@@ -566,7 +518,8 @@ __device__ __forceinline__ Smem16 stage16(const MlpArgs &M) {
 
 // host side: the dynamic LDS stage16<prec, need32> uses
 inline int smem16_bytes(const MlpArgs &M, int prec, bool need32) {
-    const bool lds32 = prec == NR_PRECISION_FP32 || (need32 && NR_LOWP_PK32_LDS);
+    (void)need32;
+    const bool lds32 = prec == NR_PRECISION_FP32;
     return (lds32 ? M.pk_bytes : 0) + (prec != NR_PRECISION_FP32 ? M.lp_bytes + M.lpf_bytes : 0);
 }
 

@@ -19,6 +19,8 @@
 //     normal work fills the tail of the frame instead of a separate launch.
 #include "nr_mlp16.h"
 
+#include <cstddef>
+
 namespace nr {
 
 // workgroups per CU the register allocation of k_trace targets (4 waves each)
@@ -68,21 +70,29 @@ typedef __attribute__((address_space(1))) uint32_t *gptr_u32;
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 
 
+// Image row of local row lr of the shard (rows are dealt in bands of A.band).
+__device__ __forceinline__ int shard_row(const RenderArgs &A, const TraceArgs &T, int lr) {
+    if (A.nshards <= 1) return lr;
+    const int bi = (int)udiv_r((uint32_t)lr, (uint32_t)A.band, T.inv_band);
+    return (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
+}
+
+// The ray direction of pixel x of local row lr (initMarcher :293-358).
+__device__ __forceinline__ F3 ray_dir(const RenderArgs &A, const TraceArgs &T, const float *M, int x, int lr) {
+    const int y = shard_row(A, T, lr);
+    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
+    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
+    F3 dd = normalize3(mk3(u, v, -2.0f));
+    return mk3(dot3(dd, mk3(M[0], M[1], M[2])), dot3(dd, mk3(M[4], M[5], M[6])), dot3(dd, mk3(M[8], M[9], M[10])));
+}
+
 // Ray generation for pixel x of local row lr of the shard (initMarcher :293-358).
 // Returns hit.
 __device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T, const float *M, int x, int lr,
                                         F3 &p, F3 &d, float &tfar) {
-    int y = lr;
-    if (A.nshards > 1) {
-        const int bi = (int)udiv_r((uint32_t)lr, (uint32_t)A.band, T.inv_band);
-        y = (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
-    }
     F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
                dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
-    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
-    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
-    F3 dd = normalize3(mk3(u, v, -2.0f));
-    dd = mk3(dot3(dd, mk3(M[0], M[1], M[2])), dot3(dd, mk3(M[4], M[5], M[6])), dot3(dd, mk3(M[8], M[9], M[10])));
+    const F3 dd = ray_dir(A, T, M, x, lr);
     float tnear;
     if (!intersect_bounding(o, dd, tnear, tfar)) return false;
     if (tnear < 0.0f) tnear = 0.0f;
@@ -90,6 +100,20 @@ __device__ __forceinline__ bool gen_ray(const RenderArgs &A, const TraceArgs &T,
     d = dd;
     return true;
 }
+
+// The per-frame values a batched k_trace keeps in LDS (FrameArgs minus the normal matrix,
+// which only the colouring reads, from global memory): 72 of 136 bytes per frame.
+struct FrameLds {
+    float inv_view[12];
+    double zoff;
+    uint32_t *out;
+    float frame_f;
+    int pad;
+};
+static_assert(sizeof(FrameLds) == 72 && offsetof(FrameLds, zoff) == 48 && offsetof(FrameLds, frame_f) == 64,
+              "FrameLds layout (staged word by word in k_trace)");
+static_assert(offsetof(FrameArgs, zoff) == 112 && offsetof(FrameArgs, out) == 120 && offsetof(FrameArgs, frame_f) == 128,
+              "FrameArgs layout (staged word by word in k_trace)");
 
 // s_setprio takes an immediate
 __device__ __forceinline__ void set_priority(int prio) {
@@ -118,14 +142,21 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
-    __shared__ FrameArgs sf[BATCH ? NR_MAX_BATCH : 1];
+    __shared__ FrameLds sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
-        const int nw = T.nframes * (int)(sizeof(FrameArgs) / 4);
-        for (int i = threadIdx.x; i < nw; i += blockDim.x)
-            reinterpret_cast<uint32_t *>(sf)[i] = reinterpret_cast<const uint32_t *>(T.frames)[i];
+        for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // 18 words per FrameLds
+            const int f = i / 18, w = i - 18 * f;
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(T.frames + f);
+            // inv_view [0, 12), zoff + out [28, 32) -> [12, 16), frame_f [32] -> 16
+            reinterpret_cast<uint32_t *>(sf + f)[w] = w < 12 ? src[w] : (w < 16 ? src[16 + w] : (w == 16 ? src[32] : 0u));
+        }
     }
     Smem16 S = stage16<PREC, true>(M);  // (its __syncthreads also covers sf)
-    __shared__ float4 stash[4][STASH][2];  // per wave: {p.xyz, pixel}, {d.xyz, -}
+    // converged rays per wave: {p.xyz, pixel} and the frame (the direction is regenerated from
+    // the pixel for facingColor; matCapColor does not read it): 21 instead of 42 KB per CU,
+    // so that 4 fp32 workgroups share a CU
+    __shared__ float4 stash[4][STASH];
+    __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -307,8 +338,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            const float4 sp = stash[wid][e][0], sd = stash[wid][e][1];
-            const int sfr = BATCH ? __float_as_int(sd.w) : 0;
+            const float4 sp = stash[wid][e];
+            const int sfr = BATCH ? (int)stash_f[wid][e] : 0;
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr_of(sfr), pq.x, pq.y, pq.z, smask);
@@ -319,8 +350,15 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
             if (k < nb && q4 == 0 && !T.itmap) {
                 const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                put(sfr, __float_as_uint(sp.w),
-                    shade_color(A, BATCH ? sf[sfr].normal : A.normal, nrm, mk3(sd.x, sd.y, sd.z)));
+                const uint32_t pxl = __float_as_uint(sp.w);
+                F3 rd = mk3(0.0f, 0.0f, 0.0f);
+                if (A.color_type == NR_COLOR_FACING) {
+                    const int lr = (int)udiv_r(pxl, (uint32_t)A.W, A.inv_w);
+                    rd = ray_dir(A, T, BATCH ? sf[sfr].inv_view : A.inv_view, (int)(pxl - (uint32_t)lr * A.W), lr);
+                }
+                const float *nmx = BATCH ? (const float *)((const __attribute__((address_space(1))) float *)T.frames[sfr].normal)
+                                         : A.normal;
+                put(sfr, pxl, shade_color(A, nmx, nrm, rd));
             }
             nconv += (uint64_t)nb;
             nstash -= nb;
@@ -401,8 +439,8 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
         const uint64_t cm = __ballot(conv);
         if (conv) {
             const int slot = nstash + (int)__popcll(cm & lanemask_lt());
-            stash[wid][slot][0] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
-            stash[wid][slot][1] = make_float4(d.x, d.y, d.z, __int_as_float(rf));
+            stash[wid][slot] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
+            if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)rf;
         }
         nstash += (int)__popcll(cm);
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; tph = t; }
