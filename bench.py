@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--geometry", default="plane_1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-frame", action="store_true")
+    ap.add_argument("--no-random-poses", action="store_true",
+                    help="skip config.random_poses (profiling passes that average the default-pose launches)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     return ap.parse_args()
 
@@ -265,8 +267,10 @@ def main():
         dt_single, _, rs_single, _, _ = timed(run_single, False)
 
     # the same timing over 8 random poses, frames cycling through them
-    dt_pose, _, rs_pose, se_pose, _ = timed(lambda n: run_batched(n, pose_cams), False)
-    pose_parity, pose_checked = check_frames(a.steps, pose_cams)
+    dt_pose = None
+    if not a.no_random_poses:
+        dt_pose, _, rs_pose, se_pose, _ = timed(lambda n: run_batched(n, pose_cams), False)
+        pose_parity, pose_checked = check_frames(a.steps, pose_cams)
 
     # roofline of the dominant kernel (k_trace) from this rank's per-launch events
     launches = max(prof["march_launches"], 1)
@@ -342,7 +346,7 @@ def main():
                 "fps": round(a.steps / dt_single, 3),
                 "schedule": "one nr_render_shard launch per frame",
             },
-            "random_poses": {
+            "random_poses": None if dt_pose is None else {
                 "value": round(rs_pose / dt_pose / 1e6, 3),
                 "ms_per_step": round(dt_pose / a.steps * 1e3, 4),
                 "fps": round(a.steps / dt_pose, 3),

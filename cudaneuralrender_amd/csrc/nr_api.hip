@@ -1138,10 +1138,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         dX = hx;
     }
     if (c->fused) {
-        // workgroups per CU: 4 for fp32; 6 for bf16/fp16, whose 122-VGPR waves (4 per SIMD)
-        // finish a 2^24-point batch 6% sooner with the extra queued workgroups
-        // (profiles/r2_mlp_lowp_dot2_prefetch.txt)
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (c->precision == NR_PRECISION_FP32 ? 4 : 6);
+        // workgroups per CU: 8 (queued beyond the resident ones, they keep every SIMD fed
+        // to the end of the batch): 2^24 points fp32 0.796 -> 0.825 of peak, bf16 (102 VGPRs,
+        // 5 waves per SIMD resident) 0.352 -> 0.410 against 4 (profiles/r2_mlp_microbench.txt)
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 8;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
