@@ -865,6 +865,12 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         const int n = std::min(chunk, nframes - f0);
         T.frames = c->d_frames + f0;
         T.nframes = n;
+        T.inv_nframes = 1.0 / (double)n;
+        // frames interleaved in 64-position chunks: every frame of the launch progresses
+        // together, so the launch does not end on one frame's silhouette rays started last
+        // (1024^2 x 32 frames 1.866 -> 1.825 ms/frame, one 8-way shard x 8 frames 0.367 ->
+        // 0.334; profiles/r2_ab_experiments.txt (10)).  Debug bit 10: frame-major (A/B).
+        T.interleave = !((c->debug >> 10) & 1);
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // 3 workgroups (12 waves) per CU once several frames share the launch: the third

@@ -90,13 +90,16 @@ struct TraceArgs {
     // takes one pixel from each of 64 blocks), so a block of long rays is marched by 64
     // different waves instead of one (0/1 = block-major)
     int spread_shift;           // log2 of the spread group (0 = block-major)
-    int itmap;
+    int itmap;                  // diagnostics: write each pixel's iteration count instead of its colour
     double inv_bw, inv_band;    // 1/bw, 1/band for udiv_r
     // cost probe (k_trace<.., true>): one ray per block
     int probe, take;
     uint64_t lane_cap;          // lanes a wave may fill: (1 << take) - 1, all 64 for take = 64
     const FrameArgs *frames;    // batched launch: nframes frames (k_trace<.., BATCH>)
-    int nframes;                  // diagnostics: write each pixel's iteration count instead of its colour
+    int nframes;
+    int interleave;             // batched: 64-position queue chunks dealt to the frames in turn
+                                // (all frames progress together) instead of frame-major
+    double inv_nframes;         // 1 / nframes for udiv_r
 };
 
 int dense_lds_bytes(int in, int out);

@@ -285,10 +285,16 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
                     if (it < 0 && rank < got) {
                         uint32_t q = base + rank;
                         int f = 0;
-                        if constexpr (BATCH) {  // frame-major: frame f owns [f * per, (f + 1) * per)
-                            const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
-                            f = (int)udiv_r(q, per, 1.0 / (double)per);
-                            q -= (uint32_t)f * per;
+                        if constexpr (BATCH) {
+                            if (T.interleave) {  // 64-position chunk c goes to frame c % n
+                                const uint32_t c = q >> 6, cq = udiv_r(c, (uint32_t)T.nframes, T.inv_nframes);
+                                f = (int)(c - cq * (uint32_t)T.nframes);
+                                q = (cq << 6) | (q & 63u);
+                            } else {  // frame-major: frame f owns [f * per, (f + 1) * per)
+                                const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
+                                f = (int)udiv_r(q, per, 1.0 / (double)per);
+                                q -= (uint32_t)f * per;
+                            }
                         }
                         uint32_t bq = q >> 6, pq = q & 63;
                         if (PROBE) {

@@ -198,7 +198,8 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
  * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = bf16 ReLU
  * by v_pk_max_i16 instead of the conversion's clamp bit (the same pack and values: parity
- * and A/B of the two forms). */
+ * and A/B of the two forms).  Bit 10 = nr_render_batch deals its pixel queue frame after
+ * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
  * next frame of the same size/shard dispenses blocks longest-first (pixels are

@@ -23,13 +23,16 @@ ap.add_argument("--size", type=int, default=1024)
 ap.add_argument("--steps", type=int, default=128)
 ap.add_argument("--spread", type=int, default=-1, help="nr_set_pixel_spread (blocks per group, -1 auto)")
 ap.add_argument("--queues", type=int, default=8, help="nr_set_queue_shards")
+ap.add_argument("--temporal", type=int, default=0, help="nr_set_temporal_order")
+ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (1024: frame-major batch queue)")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 iv, nm = nr.camera(0, 0, 2)
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
 r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
 r.set_occupancy(a.bpc).set_wave_rays(a.rays).set_schedule(a.schedule)
-r.set_pixel_spread(a.spread).set_queue_shards(a.queues)
+r.set_pixel_spread(a.spread).set_queue_shards(a.queues).set_temporal_order(a.temporal)
+r.set_debug(a.debug)
 S = a.size
 bufs = [torch.zeros(S * S, dtype=torch.int32, device="cuda") for _ in range(32)]
 for n in (int(x) for x in a.shards.split(",")):
@@ -46,4 +49,4 @@ for n in (int(x) for x in a.shards.split(",")):
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
         line.append(f"batch {b}: {dt:.3f} ms/frame")
-    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues}: " + "  ".join(line), flush=True)
+    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} debug {a.debug}: " + "  ".join(line), flush=True)
