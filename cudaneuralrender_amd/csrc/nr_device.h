@@ -178,6 +178,18 @@ __device__ float nr_sin(float xf) {
     return (float)v;
 }
 
+// The correctly rounded square root on [2^-96, FLT_MAX]: v_sqrt_f32 and the two-FMA rounding
+// correction -- the sequence hipcc emits for sqrtf, without the denormal-range scaling and
+// the zero / infinity / NaN class check that only inputs outside that range need (7 of its
+// 16 VALU).  Equal to sqrtf on every float of the domain (tools/sqrt_exhaustive.hip).
+__device__ __forceinline__ float sqrt_rn_normal(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    const float r = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : r;
+}
+
 __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
@@ -200,11 +212,24 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // wave of scattered rays nearly every sphere has some lane near it, so skipping the
     // square roots of far spheres behind a branch cost more than it saved
     // (tools/scene_bench.hip).
-    float d[9];
+    float q[9], d[9];
 #pragma unroll
     for (int row = 0; row < 3; ++row)
 #pragma unroll
-        for (int col = 0; col < 3; ++col) d[3 * row + col] = sqrtf((xx[col] + yy[row]) + zz) - 0.1f;
+        for (int col = 0; col < 3; ++col) q[3 * row + col] = (xx[col] + yy[row]) + zz;
+    // Every q is >= zz, >= min xx and >= min yy, and <= (max xx + max yy) + zz (rounding is
+    // monotone and the terms are non-negative): when the wave's bounds put all nine in
+    // sqrt_rn_normal's domain (all but points within 1e-14 of a sphere centre, or non-finite
+    // ones), the short sequence gives the same bits as sqrtf.
+    const float lo = fmaxf(zz, fmaxf(fminf(fminf(xx[0], xx[1]), xx[2]), fminf(fminf(yy[0], yy[1]), yy[2])));
+    const float hi = (fmaxf(fmaxf(xx[0], xx[1]), xx[2]) + fmaxf(fmaxf(yy[0], yy[1]), yy[2])) + zz;
+    if (__ballot(!(lo >= 0x1p-96f && hi <= 0x1.fffffep127f)) == 0) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = sqrt_rn_normal(q[i]) - 0.1f;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) d[i] = sqrtf(q[i]) - 0.1f;
+    }
     float s = nsdf;
 #pragma unroll
     for (int i = 0; i < 9; ++i) s = smooth_union(s, d[i], 0.01f);
