@@ -58,15 +58,24 @@ def _worker(rank, world, port, band, W, H, nframes, result_path):
             shards = [src[s * nframes * shard_px: s * nframes * shard_px + shard_px].reshape(max_rows, W)
                       for s in range(world)]
             out.append(nr.assemble_shards(shards, W, H, band, world))
+        if H % (band * world) == 0:
+            # bench.py's single assembly: when every frame is a whole number of band rounds,
+            # the n frames stacked are one (n*H)-row image whose shard s is rank s's gathered
+            # n x max_rows rows
+            stacked = [flat[s * nframes * shard_px:(s + 1) * nframes * shard_px].reshape(nframes * max_rows, W)
+                       for s in range(world)]
+            one = nr.assemble_shards(stacked, W, nframes * H, band, world).reshape(nframes, H, W)
+            assert np.array_equal(one, np.stack(out))
         np.save(result_path, np.stack([np.stack(out), np.stack(fulls)]))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band,nframes", [(2, 8, 1), (3, 5, 1), (2, 8, 3), (3, 1, 2), (2, 1, 3)])
-def test_gloo_gather_assemble(tmp_path, world, band, nframes):
+@pytest.mark.parametrize("world,band,nframes,H", [(2, 8, 1, 41), (3, 5, 1, 41), (2, 8, 3, 41), (3, 1, 2, 41),
+                                                (2, 1, 3, 41), (2, 1, 3, 48), (3, 1, 4, 48), (2, 8, 2, 48)])
+def test_gloo_gather_assemble(tmp_path, world, band, nframes, H):
     import torch.multiprocessing as mp
-    W, H = 48, 41
+    W = 48
     out = str(tmp_path / "res.npy")
     mp.spawn(_worker, args=(world, _free_port(), band, W, H, nframes, out), nprocs=world, join=True)
     frames, fulls = np.load(out)

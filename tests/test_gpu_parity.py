@@ -154,6 +154,36 @@ def test_shards_assemble_to_frame(rend, nets, chrome, nshards, band):
     assert np.array_equal(nr.assemble_shards(shards, W, H, band, nshards), full)
 
 
+@pytest.mark.parametrize("nshards,band", [(2, 1), (4, 1), (8, 1), (2, 4)])
+def test_stacked_assembly_device(rend, nets, chrome, nshards, band):
+    """bench.py's N-rank collection on one device: each shard's n frames rendered by one
+    nr_render_batch into a rank-major buffer (the layout one RCCL gather leaves on rank 0),
+    then ONE device nr_assemble_shards of the n frames stacked as an (n*H)-row image (valid
+    when H is a multiple of band * nshards) -- equal to the single-GPU frames."""
+    import torch
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    W, H, n = 96, 64, 5
+    assert H % (band * nshards) == 0
+    cams = [(*nr.camera(-10.0, 30.0 * i, 2.0), 0) for i in range(n)]
+    rows = H // nshards
+    gather = torch.zeros(nshards, n * rows * W, dtype=torch.int32, device="cuda")
+    frames = torch.zeros(n, H * W, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # torch's fills before libnr's (non-blocking) stream writes
+    for s in range(nshards):
+        assert nr.shard_rows(H, band, nshards, s) == rows
+        rend.render_batch_device([gather[s].data_ptr() + i * rows * W * 4 for i in range(n)], W, H, cams, 128, band,
+                                 nshards, s)
+    rend.assemble_device(gather.data_ptr(), n * rows * W, frames.data_ptr(), W, n * H, band, nshards)
+    rend.synchronize()
+    got = frames.cpu().numpy().view(np.uint32).reshape(n, H, W)
+    for i, (iv, nm, f) in enumerate(cams):
+        rend.set_view(iv, nm, f)
+        ref, _ = rend.render(W, H, 128)
+        assert np.array_equal(got[i], ref), i
+    rend.set_view(*nr.camera(0, 0, 2), 0)
+
+
 @pytest.mark.parametrize("prec,tol", [("bf16", 0.05), ("fp16", 0.01)])
 def test_mlp_lowp_tolerance(rend, nets, golden, prec, tol):
     dims, K, B = nets["plane_1"]
