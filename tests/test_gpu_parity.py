@@ -160,23 +160,29 @@ def test_stacked_assembly_device(rend, nets, chrome, nshards, band):
     nr_render_batch into a rank-major buffer (the layout one RCCL gather leaves on rank 0),
     then ONE device nr_assemble_shards of the n frames stacked as an (n*H)-row image (valid
     when H is a multiple of band * nshards) -- equal to the single-GPU frames."""
-    import torch
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")  # libnr's HIP runtime (by soname): device buffers without torch
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision("fp32").set_static(1, 3).set_scene("v1").set_matcap(chrome)
     W, H, n = 96, 64, 5
     assert H % (band * nshards) == 0
     cams = [(*nr.camera(-10.0, 30.0 * i, 2.0), 0) for i in range(n)]
     rows = H // nshards
-    gather = torch.zeros(nshards, n * rows * W, dtype=torch.int32, device="cuda")
-    frames = torch.zeros(n, H * W, dtype=torch.int32, device="cuda")
-    torch.cuda.synchronize()  # torch's fills before libnr's (non-blocking) stream writes
-    for s in range(nshards):
-        assert nr.shard_rows(H, band, nshards, s) == rows
-        rend.render_batch_device([gather[s].data_ptr() + i * rows * W * 4 for i in range(n)], W, H, cams, 128, band,
-                                 nshards, s)
-    rend.assemble_device(gather.data_ptr(), n * rows * W, frames.data_ptr(), W, n * H, band, nshards)
-    rend.synchronize()
-    got = frames.cpu().numpy().view(np.uint32).reshape(n, H, W)
+    gather, frames = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(gather), ctypes.c_size_t(nshards * n * rows * W * 4)) == 0
+    assert hip.hipMalloc(ctypes.byref(frames), ctypes.c_size_t(n * H * W * 4)) == 0
+    try:
+        for s in range(nshards):
+            assert nr.shard_rows(H, band, nshards, s) == rows
+            base = gather.value + s * n * rows * W * 4
+            rend.render_batch_device([base + i * rows * W * 4 for i in range(n)], W, H, cams, 128, band, nshards, s)
+        rend.assemble_device(gather.value, n * rows * W, frames.value, W, n * H, band, nshards)
+        rend.synchronize()
+        got = np.zeros((n, H, W), np.uint32)
+        assert hip.hipMemcpy(ctypes.c_void_p(got.ctypes.data), frames, ctypes.c_size_t(got.nbytes), 2) == 0  # D2H
+    finally:
+        hip.hipFree(gather)
+        hip.hipFree(frames)
     for i, (iv, nm, f) in enumerate(cams):
         rend.set_view(iv, nm, f)
         ref, _ = rend.render(W, H, 128)
