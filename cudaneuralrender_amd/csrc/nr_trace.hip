@@ -481,7 +481,9 @@ template <int PREC>
 __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
-    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // the wave's chunk index is uniform: readfirstlane keeps the loop control (base, rem,
+    // tmask) in SGPRs instead of 64-bit VALU arithmetic on every lane
+    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const long stride = (((long)gridDim.x * blockDim.x) >> 6) * 64;
     auto load = [&](long i, float &x, float &y, float &z, float &f) {
         x = y = z = f = 0.0f;
@@ -495,6 +497,8 @@ __global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__rest
     float nx, ny, nz, nf;
     load(base + lane, nx, ny, nz, nf);
     for (; base < n; base += stride) {
+        base = (long)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)base));  // uniform: SGPRs
         const long i = base + lane;
         const float x = nx, y = ny, z = nz, f = nf;
         load(base + stride + lane, nx, ny, nz, nf);
