@@ -8,9 +8,9 @@ device memory (and, for N > 1, gathered to rank 0 and assembled).
 
     python bench.py [--gpus N --steps K --warmup W]
 The K frames of the timed region go through nr_render_batch: the persistent tracer's
-pixel queue runs through the frames in order (up to 32 per launch), so one frame's
-longest rays march while the next frame's pixels keep the matrix cores busy -- every
-frame is rendered in full, none is reused.  config.single_frame repeats the timing with
+pixel queue deals 64-pixel chunks to the frames in turn (up to 32 frames per launch), so
+one frame's longest rays march while other frames' pixels keep the matrix cores busy --
+every frame is rendered in full, none is reused.  config.single_frame repeats the timing with
 one nr_render call per frame (each launch waits for the previous frame's last ray).
 
 N > 1 runs one rank per GPU under torch.distributed.run: the driver's launcher, or, when
@@ -339,8 +339,8 @@ def main():
             "ray_steps_per_frame": int(ray_steps_k / a.steps),
             "shade_evals_per_frame": int(shade_evals_k / a.steps),
             "frames_per_launch": min(a.steps, MAX_BATCH),
-            "schedule": "nr_render_batch: the K timed frames through one frame-major pixel queue "
-                        "(every frame rendered in full)",
+            "schedule": "nr_render_batch: the K timed frames through one pixel queue, 64-pixel chunks "
+                        "dealt to the frames in turn (every frame rendered in full)",
             "parallelism": f"row-band shards x{world} (band {BAND}) + one RCCL gather per batch of frames"
                            if world > 1 else "single GPU",
             "parity_vs_single_gpu_render": parity,
