@@ -45,7 +45,9 @@ struct nr_ctx {
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
-    bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16 on the same pack
+    bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
+                            // on the same packs
+    bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
     int debug = 0;
@@ -223,8 +225,11 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
         HIPCHK(c, hipMemcpy(db, c->biases[l].data(), (size_t)out * 4, hipMemcpyHostToDevice));
     }
     std::vector<float> pack16;
-    c->fused = pack_fp32_16(c->dims, c->kernels, c->biases, pack16);
+    int f32_clamp = 0;
+    c->fused = pack_fp32_16(c->dims, c->kernels, c->biases, pack16, &f32_clamp);
     c->mlp16 = MlpArgs{};
+    c->f32_clamp_ok = c->fused && f32_clamp != 0;
+    c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;
     if (c->fused) {
         size_t pb = (pack16.size() * 4 + 15) / 16 * 16;
         pack16.resize(pb / 4, 0.0f);
@@ -1297,6 +1302,7 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
+    c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;
     return NR_OK;
 }
 

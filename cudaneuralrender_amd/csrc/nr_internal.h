@@ -35,7 +35,7 @@ int report_error(int code, const char *fmt, ...) __attribute__((format(printf, 2
 //   per hidden layer j (0..nh-1), base 160 + j*1056:
 //              A operand           [m >> 2][lane 64][m & 3]   (m = 2 * k-step + row tile)
 //              bias                [group 4][register 8]
-//   final:     weights [group 4][register 8], bias [1] (+3 pad)
+//   final:     weights [group 4][register 8], bias [1], layer-0 output scale 2^-e0 [1] (+2 pad)
 constexpr int PK_L0W = 0;
 constexpr int PK_L0B = 128;
 constexpr int PK_HID = 160;
@@ -63,12 +63,18 @@ NR_HD constexpr inline int lp32_floats(int nh) { return 32 + 32 * nh + 4; }
 // bf16 clamped-ReLU pack: every network input within +-LP_INPUT_BOUND keeps every scaled
 // activation at or below 1/4 (interval bounds, nr_pack.cpp pack_lowp_32)
 constexpr float LP_INPUT_BOUND = 1048576.0f;
+// fp32 clamped-ReLU pack (pack_fp32_16): inputs within +-F32_INPUT_BOUND keep every scaled
+// activation at or below 1/2, and inputs of magnitude below F32_INPUT_TINY (other than 0)
+// take the max-ReLU form too (nr_mlp16.h inputs_in_bound_f32)
+constexpr float F32_INPUT_BOUND = 1024.0f;
+constexpr float F32_INPUT_TINY = 0x1p-60f;
 
 bool fused_shape_ok(const std::vector<int> &dims);
 // Keras kernels (in x out, row-major) -> packs.  Return false if the shape is not
 // [3|4, 32, ..., 32, 1] (those networks render on the layered schedule).
+// pack_fp32_16: clamp (if not null) = 1 when the pack is scaled for the clamped ReLU
 bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
-                  const std::vector<std::vector<float>> &biases, std::vector<float> &pack);
+                  const std::vector<std::vector<float>> &biases, std::vector<float> &pack, int *clamp = nullptr);
 bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, int precision,
                   std::vector<uint16_t> &a_ops, std::vector<float> &bias, int *clamp = nullptr);

@@ -14,6 +14,8 @@ struct MlpArgs {
     int in0, nh;
     int lp_clamp;           // bf16 pack scaled for the clamped ReLU (nr_pack.cpp): valid for
                             // inputs within LP_INPUT_BOUND; the launch clears it otherwise
+    int f32_clamp;          // fp32 pack scaled for the clamped ReLU (pack_fp32_16): used by the
+                            // waves whose inputs are all within F32_INPUT_BOUND
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,

@@ -537,7 +537,7 @@ __global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, QueueA
         const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
         const long rem = n_s - off;  // rays; 4 per 16-point tile
         const uint32_t tmask = rem >= 16 ? 0xfu : (1u << ((rem + 3) >> 2)) - 1u;
-        const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, F[f].frame_f, pq.x, pq.y, pq.z, tmask);
+        const float sdf = mlp16_fp32(M, S.s32, F[f].frame_f, pq.x, pq.y, pq.z, tmask);
         shade_rays(A, F[f].normal, F[f].out, F[f].zoff, live, sp, sd, tag & WF_PMASK, sdf);
     }
 }

@@ -29,9 +29,15 @@ __device__ __forceinline__ float tile_outputs(const float zt[4]) {
 
 // FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
 // PART != 0 only in the latency diagnostic (nr_diag.hip): stop after the hidden layers.
-template <int NT, int PART = 0>
+// CL: bias add and ReLU as one v_add_f32 / v_fma_f32 with the clamp bit (clamp to [0, 1]),
+// valid on the scaled pack (nr_pack.cpp pack_fp32_16) for inputs within F32_INPUT_BOUND,
+// where every activation is at most 1/2: bit-equal to fmaxf(v, 0) (NaN and -0 aside, which
+// the chains of the next layer map to the same values).  Every VALU instruction costs f32
+// matrix time on gfx950 (profiles/r1_mfma_peak.txt), and this halves the activation VALU.
+template <int NT, int PART = 0, bool CL = false>
 __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
                                                float y, float z) {
+    auto relu = [](float v) { return CL ? __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f) : fmaxf(v, 0.0f); };
     // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
     const int lane = lane_id(), g = lane >> 4, j = lane & 15;
     float a[NT][8];
@@ -52,12 +58,15 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
         const float4 *bb = reinterpret_cast<const float4 *>(s + PK_L0B + g * 8);
         const float4 blo = bb[0], bhi = bb[1];
         const float bias[8] = {blo.x, blo.y, blo.z, blo.w, bhi.x, bhi.y, bhi.z, bhi.w};
+        // the layer-0 weights are unscaled; fma(c, 2^-e0, b 2^-e0) = (c + b) 2^-e0 in one
+        // rounding (2^-e0 = 1 on an unscaled pack: c + b)
+        const float s0 = s[pk_final(nh) + 33];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
+                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = relu(__builtin_fmaf(c[t][mt][r], s0, bias[4 * mt + r]));
     }
     // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
     for (int jl = 0; jl < nh; ++jl) {
@@ -86,7 +95,7 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = fmaxf(c[t][mt][r] + bias[4 * mt + r], 0.0f);
+                for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = relu(c[t][mt][r] + bias[4 * mt + r]);
     }
     if constexpr (PART != 0) return a[0][0] + a[NT - 1][7];
     if constexpr (NT >= 3) {
@@ -150,13 +159,39 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
     return tile_outputs(zt);
 }
 
+// wave-uniform: every lane's inputs are within F32_INPUT_BOUND (NaN is not)
+__device__ __forceinline__ bool inputs_in_bound_f32(float x, float y, float z, float f) {
+    const bool ok = __builtin_fabsf(x) <= F32_INPUT_BOUND && __builtin_fabsf(y) <= F32_INPUT_BOUND &&
+                    __builtin_fabsf(z) <= F32_INPUT_BOUND && __builtin_fabsf(f) <= F32_INPUT_BOUND;
+    return __ballot(!ok) == 0;
+}
+
+// fp32 ReLU form: NR_F32_CLAMP 0 builds the add + max form only (A/B)
+#ifndef NR_F32_CLAMP
+#define NR_F32_CLAMP 1
+#endif
+// cl (wave-uniform): the pack is scaled (MlpArgs::f32_clamp) and the inputs are within the
+// bound -- the clamped form on the active tiles; otherwise (never on the bundled networks'
+// rays) the add + max form on all four tiles, which keeps one extra copy of the MLP code
+// in the kernels instead of four
 __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
-                                            float z, uint32_t tmask) {
+                                            float z, uint32_t tmask, bool cl) {
     const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
+    if (NR_F32_CLAMP && cl) {
+        if (nt >= 4) return mlp16_fp32_nt<4, 0, true>(s, in0, nh, fr, x, y, z);
+        if (nt == 3) return mlp16_fp32_nt<3, 0, true>(s, in0, nh, fr, x, y, z);
+        if (nt == 2) return mlp16_fp32_nt<2, 0, true>(s, in0, nh, fr, x, y, z);
+        return mlp16_fp32_nt<1, 0, true>(s, in0, nh, fr, x, y, z);
+    }
+    if (NR_F32_CLAMP) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
     if (nt >= 4) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
     if (nt == 3) return mlp16_fp32_nt<3>(s, in0, nh, fr, x, y, z);
     if (nt == 2) return mlp16_fp32_nt<2>(s, in0, nh, fr, x, y, z);
     return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
+}
+__device__ __forceinline__ float mlp16_fp32(const MlpArgs &M, const float *s, float fr, float x, float y, float z,
+                                            uint32_t tmask) {
+    return mlp16_fp32(s, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
 }
 
 // bf16 / fp16: the whole MLP on 32-point tiles, v_mfma_f32_32x32x16_{bf16,f16} (nr_internal.h
@@ -461,7 +496,7 @@ __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
     if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
-    return mlp16_fp32(s32, M.in0, M.nh, fr, x, y, z, tmask);
+    return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }
 
 // wave-uniform: every lane's inputs are within LP_INPUT_BOUND (NaN is not)

@@ -62,6 +62,65 @@ float fp16f(uint16_t h) {
 }
 }  // namespace
 
+// Power-of-two scales for the clamped-ReLU packs: e[l] such that every ReLU layer l's
+// activation, for network inputs within +-bound, is at most 2^e[l] / 2^margin.  Interval
+// arithmetic in double over the exact f32 weights; the margin covers the rounding of the
+// evaluation (bf16: 2 -- weights and activations rounded to bf16, relative 2^-9 each per
+// layer, ~3% over 8 layers; fp32: 1 -- f32 chains, ~2^-19 relative).  Returns false when a
+// scale or a scaled weight would leave the range where power-of-two scaling is exact.
+static bool clamp_scales(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                         const std::vector<std::vector<float>> &B, std::vector<int> &e, double bound, int margin) {
+    const int nl = (int)dims.size() - 1;
+    std::vector<double> lo(dims[0], -bound), hi(dims[0], bound);
+    e.assign(nl - 1, 0);
+    for (int l = 0; l < nl - 1; ++l) {
+        const int in = dims[l], out = dims[l + 1];
+        std::vector<double> nlo(out), nhi(out);
+        double top = 0.0;
+        for (int u = 0; u < out; ++u) {
+            double a = B[l][u], b = B[l][u];
+            for (int i = 0; i < in; ++i) {
+                const double w = K[l][(size_t)i * out + u];
+                a += std::min(w * lo[i], w * hi[i]);
+                b += std::max(w * lo[i], w * hi[i]);
+            }
+            nlo[u] = std::max(a, 0.0);  // ReLU
+            nhi[u] = std::max(b, 0.0);
+            top = std::max(top, nhi[u]);
+        }
+        if (!std::isfinite(top)) return false;
+        e[l] = top > 0.0 ? (int)std::ceil(std::log2(top)) + margin : 0;
+        if (e[l] < -60 || e[l] > 100) return false;
+        lo = nlo;
+        hi = nhi;
+    }
+    // every scaled nonzero weight and bias must stay a normal bf16 / f32 well inside range
+    for (int l = 0; l < nl; ++l) {
+        const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
+        const int sb = l < nl - 1 ? -e[l] : 0;
+        for (float w : K[l])
+            if (w != 0.0f && (std::fabs(std::ldexp((double)w, sw)) < 0x1p-110 || std::fabs(std::ldexp((double)w, sw)) > 0x1p110))
+                return false;
+        for (float b : B[l])
+            if (b != 0.0f && (std::fabs(std::ldexp((double)b, sb)) < 0x1p-110 || std::fabs(std::ldexp((double)b, sb)) > 0x1p110))
+                return false;
+    }
+    return true;
+}
+
+// Layer l's weights times 2^(e[l-1] - e[l]) and its bias times 2^-e[l] (e[-1] = 0, e[last]
+// = 0): activations come out scaled by 2^-e[l] and the last layer's output unscaled.
+static void apply_scales(const std::vector<int> &e, std::vector<std::vector<float>> &K,
+                         std::vector<std::vector<float>> &B) {
+    const int nl = (int)K.size();
+    for (int l = 0; l < nl; ++l) {
+        const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
+        const int sb = l < nl - 1 ? -e[l] : 0;
+        for (float &w : K[l]) w = std::ldexp(w, sw);
+        for (float &b : B[l]) b = std::ldexp(b, sb);
+    }
+}
+
 // ---- 16-point tiles (nr_mlp16.h).  Lane (j, g): point j, unit group g; register k.
 namespace {
 // fp32: unit held by (g, k): next layer MFMA -> 4k + g (ascending f32 chain over the
@@ -69,11 +128,31 @@ namespace {
 inline int unit16(int g, int k, bool final_consumer) { return final_consumer ? 8 * g + k : 4 * k + g; }
 }  // namespace
 
-bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-                  const std::vector<std::vector<float>> &B, std::vector<float> &pack) {
+// The fp32 pack is scaled like the bf16 clamped pack (clamp_scales, F32_INPUT_BOUND): each
+// f32 product, fmaf chain and bias add then computes its unscaled value times 2^-e exactly
+// (rounding is scale-invariant while values stay normal), so the network's output is the
+// unscaled network's bit for bit, and ReLU activations stay <= 1/2 for inputs within the
+// bound -- v_add_f32 with the clamp bit is then the bias add and the ReLU in one
+// instruction (nr_mlp16.h).  (An intermediate value of the unscaled network below
+// 2^(e - 126) in magnitude, e <= ~27 for the bundled networks, would round differently
+// once scaled; nonzero values of a bounded-input network sit at the bias/weight scale,
+// ~1e-10 and above, and the kernels send inputs below F32_INPUT_TINY to the max form.)
+bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &Kin,
+                  const std::vector<std::vector<float>> &Bin, std::vector<float> &pack, int *clamp) {
     if (!fused_shape_ok(dims)) return false;
     int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    std::vector<int> e;
+    const bool cl = clamp_scales(dims, Kin, Bin, e, (double)F32_INPUT_BOUND, 1);
+    if (clamp) *clamp = cl ? 1 : 0;
+    std::vector<std::vector<float>> K(Kin), B(Bin);
+    if (cl) {
+        apply_scales(e, K, B);
+        // layer 0 keeps its f32 weights (the products of the raw inputs are the reference's);
+        // its chain is scaled on the way out: fma(c, 2^-e0, b 2^-e0) = (c + b) 2^-e0
+        K[0] = Kin[0];
+    }
     pack.assign(pk_floats(nh), 0.0f);
+    pack[pk_final(nh) + 33] = cl ? std::ldexp(1.0f, -e[0]) : 1.0f;
     // layer 0 as one 16x16x4 MFMA per row tile: A[row 16mt + i][k = input kk]
     for (int mt = 0; mt < 2; ++mt)
         for (int lane = 0; lane < 64; ++lane) {
@@ -108,51 +187,6 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
     return true;
 }
 
-// Power-of-two scales for the bf16 clamped-ReLU pack: e[l] such that every ReLU layer l's
-// activation, for network inputs within +-LP_INPUT_BOUND, is at most 2^e[l] / 4.  Interval
-// arithmetic in double over the exact f32 weights; the factor 4 covers the bf16 rounding of
-// weights and activations (relative 2^-9 each per layer, ~3% over 8 layers).  Returns false
-// when a scale or a scaled weight would leave the range where bf16 scaling is exact.
-static bool clamp_scales(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-                         const std::vector<std::vector<float>> &B, std::vector<int> &e) {
-    const int nl = (int)dims.size() - 1;
-    std::vector<double> lo(dims[0], -(double)LP_INPUT_BOUND), hi(dims[0], (double)LP_INPUT_BOUND);
-    e.assign(nl - 1, 0);
-    for (int l = 0; l < nl - 1; ++l) {
-        const int in = dims[l], out = dims[l + 1];
-        std::vector<double> nlo(out), nhi(out);
-        double top = 0.0;
-        for (int u = 0; u < out; ++u) {
-            double a = B[l][u], b = B[l][u];
-            for (int i = 0; i < in; ++i) {
-                const double w = K[l][(size_t)i * out + u];
-                a += std::min(w * lo[i], w * hi[i]);
-                b += std::max(w * lo[i], w * hi[i]);
-            }
-            nlo[u] = std::max(a, 0.0);  // ReLU
-            nhi[u] = std::max(b, 0.0);
-            top = std::max(top, nhi[u]);
-        }
-        if (!std::isfinite(top)) return false;
-        e[l] = top > 0.0 ? (int)std::ceil(std::log2(top)) + 2 : 0;
-        if (e[l] < -60 || e[l] > 100) return false;
-        lo = nlo;
-        hi = nhi;
-    }
-    // every scaled nonzero weight and bias must stay a normal bf16 / f32 well inside range
-    for (int l = 0; l < nl; ++l) {
-        const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
-        const int sb = l < nl - 1 ? -e[l] : 0;
-        for (float w : K[l])
-            if (w != 0.0f && (std::fabs(std::ldexp((double)w, sw)) < 0x1p-110 || std::fabs(std::ldexp((double)w, sw)) > 0x1p110))
-                return false;
-        for (float b : B[l])
-            if (b != 0.0f && (std::fabs(std::ldexp((double)b, sb)) < 0x1p-110 || std::fabs(std::ldexp((double)b, sb)) > 0x1p110))
-                return false;
-    }
-    return true;
-}
-
 bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &Kin,
                   const std::vector<std::vector<float>> &Bin, int precision, std::vector<uint16_t> &a_ops,
                   std::vector<float> &fl, int *clamp) {
@@ -164,16 +198,10 @@ bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<fl
     // unscaled: power-of-two scaling is exact in bf16 and f32, so the network computes the same
     // values as unscaled, and activations stay below 1 for the clamped ReLU (nr_mlp16.h)
     std::vector<int> e;
-    const bool cl = bf && clamp_scales(dims, Kin, Bin, e);
+    const bool cl = bf && clamp_scales(dims, Kin, Bin, e, (double)LP_INPUT_BOUND, 2);
     if (clamp) *clamp = cl ? 1 : 0;
     std::vector<std::vector<float>> K(Kin), B(Bin);
-    if (cl)
-        for (int l = 0; l < nl; ++l) {
-            const int sw = (l > 0 ? e[l - 1] : 0) - (l < nl - 1 ? e[l] : 0);
-            const int sb = l < nl - 1 ? -e[l] : 0;
-            for (float &w : K[l]) w = std::ldexp(w, sw);
-            for (float &b : B[l]) b = std::ldexp(b, sb);
-        }
+    if (cl) apply_scales(e, K, B);
     auto cvt = [&](float v) { return bf ? f2bf16(v) : f2fp16(v); };
     auto back = [&](uint16_t h) { return bf ? bf16f(h) : fp16f(h); };
     auto lo = [&](float v) { return cvt(v - back(cvt(v))); };  // the residual's 16-bit value

@@ -137,7 +137,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // frame-dependent values (camera, sphere offset, animation input, output image) come
 // from the FrameArgs staged in LDS.
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
-__global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, (PREC == NR_PRECISION_FP32 && BATCH) ? 4 : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256, NR_TRACE_BPC) void k_trace(RenderArgs A, MlpAr
             const int sfr = BATCH ? (int)stash_f[wid][e] : 0;
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
-            const float sdf = mlp16_fp32(S.s32, M.in0, M.nh, fr_of(sfr), pq.x, pq.y, pq.z, smask);
+            const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
             const int l0 = lane & ~3;
             const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));

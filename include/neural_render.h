@@ -196,9 +196,10 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
  * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
  * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
- * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = bf16 ReLU
- * by v_pk_max_i16 instead of the conversion's clamp bit (the same pack and values: parity
- * and A/B of the two forms).  Bit 10 = nr_render_batch deals its pixel queue frame after
+ * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = the plain ReLU
+ * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
+ * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and
+ * A/B of the two forms).  Bit 10 = nr_render_batch deals its pixel queue frame after
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the

@@ -1,0 +1,96 @@
+"""fp32 clamped ReLU (nr_mlp16.h mlp16_fp32_nt<.., CL>): on the power-of-two-scaled fp32 pack
+(nr_pack.cpp pack_fp32_16) the bias add and the ReLU are one v_add_f32 / v_fma_f32 with the
+clamp bit.  The network output is the unscaled network's bit for bit, so every fp32 parity
+test against the oracle covers it; these tests add the inputs beyond F32_INPUT_BOUND (the
+kernel's add + max form on the same pack) and the A/B against that form (nr_set_debug
+bit 9) on every render path."""
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+from conftest import GEOMS
+
+pytestmark = pytest.mark.gpu
+NO_CLAMP = 1 << 9
+
+
+@pytest.fixture(scope="module")
+def rend():
+    r = nr.Renderer(0)
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def chrome():
+    return nr.load_png(nr.matcap_path("Chrome"))
+
+
+def both(rend, fn):
+    """fn() with the clamped ReLU, then with add + max (debug bit 9)."""
+    rend.set_debug(0)
+    a = fn()
+    rend.set_debug(NO_CLAMP)
+    try:
+        b = fn()
+    finally:
+        rend.set_debug(0)
+    return a, b
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_mlp_clamp_bitexact_with_fallback(rend, nets, geom):
+    dims, K, B = nets[geom]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    rng = np.random.default_rng(11)
+    X = rng.uniform(-1.5, 1.5, size=(30000, 3)).astype(np.float32)
+    X[777] = (3000.0, 0.0, 0.0)   # its 64-point chunk exceeds F32_INPUT_BOUND: add + max form
+    X[20000:20100] *= 600.0        # large but within the bound: clamped form
+    X[25000:25064] = 0.0           # zero inputs (the chains' +0 start)
+    a, b = both(rend, lambda: rend.mlp_forward(X))
+    ref = oracle.OracleNet(K, B).forward(X)
+    assert np.array_equal(a, ref), np.abs(a - ref).max()
+    assert np.array_equal(b, ref)
+
+
+@pytest.mark.parametrize("schedule", ["persistent", "wavefront"])
+def test_render_clamp_equals_max(rend, nets, chrome, schedule):
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_schedule(schedule)
+    rend.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+    rng = np.random.default_rng(12)
+    cams = [(*nr.camera(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360)), 2.0), 0) for _ in range(4)]
+    try:
+        (ia, sa), (ib, sb) = both(rend, lambda: rend.render_batch(96, 80, cams, 128))
+        assert all(np.array_equal(x, y) for x, y in zip(ia, ib))
+        assert sa["ray_steps"] == sb["ray_steps"] and sa["rays_shaded"] == sb["rays_shaded"]
+        rend.set_view(*cams[0])
+        (fa, _), (fb, _) = both(rend, lambda: rend.render(96, 80, 128))
+        assert np.array_equal(fa, fb) and np.array_equal(fa, ia[0])
+        iv, nm, _ = cams[0]
+        ref, _ = oracle.OracleNet(K, B).render(96, 80, iv, nm, color_type=1, matcap=chrome, max_steps=128)
+        assert np.array_equal(fa, ref)
+    finally:
+        rend.set_schedule("persistent").set_view(*nr.camera(0, 0, 2), 0)
+
+
+def test_animation_frame_beyond_bound(rend):
+    """A 4-input network: a frame number beyond F32_INPUT_BOUND sends every wave to the
+    add + max form; both frames bit-exact with the oracle."""
+    rng = np.random.default_rng(13)
+    dims = [4] + [32] * 8 + [1]
+    K = [(rng.standard_normal((dims[i], dims[i + 1])) * (1.0 / np.sqrt(dims[i]))).astype(np.float32) for i in range(9)]
+    B = [(rng.standard_normal(dims[i + 1]) * 0.05).astype(np.float32) for i in range(9)]
+    B[-1][0] = 0.3
+    rend.load_mlp(dims, K, B).set_precision("fp32").set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
+    iv, nm = nr.camera(10.0, 20.0, 2.0)
+    try:
+        for frame in (7, 5000):
+            rend.set_view(iv, nm, frame)
+            img, _ = rend.render(64, 48, 64)
+            ref, _ = oracle.OracleNet(K, B).render(64, 48, iv, nm, frame=frame, color_type=nr.NR_COLOR_FACING,
+                                                   num_inputs=4, max_steps=64)
+            assert np.array_equal(img, ref), frame
+    finally:
+        rend.set_static(nr.NR_COLOR_MATCAP, 3).set_view(*nr.camera(0, 0, 2), 0)
