@@ -27,6 +27,10 @@ namespace nr {
 #ifndef NR_TRACE_BPC
 #define NR_TRACE_BPC 3
 #endif
+// the batched fp32 instance: 4 workgroups per CU (<= 128 VGPRs) for launches of >= 8 M pixels
+#ifndef NR_TRACE_BPC_F32_BATCH
+#define NR_TRACE_BPC_F32_BATCH 4
+#endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
@@ -137,7 +141,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // frame-dependent values (camera, sphere offset, animation input, output image) come
 // from the FrameArgs staged in LDS.
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
-__global__ __launch_bounds__(256, (PREC == NR_PRECISION_FP32 && BATCH) ? 4 : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, (PREC == NR_PRECISION_FP32 && BATCH) ? NR_TRACE_BPC_F32_BATCH : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
