@@ -44,16 +44,26 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
     f32x4 c[NT][2];
     // layer 0 on the matrix core too: K = in0 padded to 4 (weight 0 for the pad, whose
     // fma adds +0 to a chain that can never be -0), one v_mfma_f32_16x16x4_f32 per
-    // row tile.  Lane (j, g) feeds input g of point j.
+    // row tile.  Lane (j, g) of tile t's B operand feeds input g of point 16t + j: the
+    // 4x4 transpose of (input, tile) lane-group blocks of {x, y, z, frame} -- four
+    // v_permlane{32,16}_swap instead of 16 ds_bpermute and 12 selects.
     {
         const float w0 = s[PK_L0W + lane], w1 = s[PK_L0W + 64 + lane];
+        uint32_t t0 = __float_as_uint(x), t1 = __float_as_uint(y), t2 = __float_as_uint(z);
+        uint32_t t3 = __float_as_uint(in0 == 4 ? fr : 0.0f);
+        auto r = __builtin_amdgcn_permlane32_swap(t0, t2, false, false);  // groups 2,3 <-> 0,1
+        t0 = r[0]; t2 = r[1];
+        r = __builtin_amdgcn_permlane32_swap(t1, t3, false, false);
+        t1 = r[0]; t3 = r[1];
+        r = __builtin_amdgcn_permlane16_swap(t0, t1, false, false);       // groups 1,3 <-> 0,2
+        t0 = r[0]; t1 = r[1];
+        r = __builtin_amdgcn_permlane16_swap(t2, t3, false, false);
+        t2 = r[0]; t3 = r[1];
+        const float bt[4] = {__uint_as_float(t0), __uint_as_float(t1), __uint_as_float(t2), __uint_as_float(t3)};
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-            const float px = __shfl(x, 16 * t + j), py = __shfl(y, 16 * t + j), pz = __shfl(z, 16 * t + j);
-            const float pw = in0 == 4 ? __shfl(fr, 16 * t + j) : 0.0f;
-            const float b = g == 0 ? px : (g == 1 ? py : (g == 2 ? pz : pw));
-            c[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
-            c[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, b, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+            c[t][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0, bt[t], f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
+            c[t][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(w1, bt[t], f32x4{0.0f, 0.0f, 0.0f, 0.0f}, 0, 0, 0);
         }
         const float4 *bb = reinterpret_cast<const float4 *>(s + PK_L0B + g * 8);
         const float4 blo = bb[0], bhi = bb[1];
