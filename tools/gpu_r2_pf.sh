@@ -1,10 +1,14 @@
+# fp32 next-layer A-operand prefetch in the 1-2 tile MLP variants: lone-wave MLP latency,
+# single-frame and 8-shard frame times, A/B against build/prev
 set -o pipefail
 mkdir -p gpurun_out
-ALT=build/alt_nopf/libnr.so
-timeout -k 10 300 python -u -m pytest tests/test_gpu_lowp.py tests/test_gpu_parity.py -k "lowp or clamp" -x -q --timeout 200 --timeout-method thread > gpurun_out/pf_tests.log 2>&1 && \
-for i in 1 2; do
-timeout -k 10 200 python -u tools/mlp_bench.py --precision bf16,fp16 --bpc 3,4,6 --iters 10 --n 16777216 >> gpurun_out/mlp_pf.log 2>&1 && \
-NR_LIBRARY=$ALT timeout -k 10 200 python -u tools/mlp_bench.py --precision bf16,fp16 --bpc 3,4,6 --iters 10 --n 16777216 | sed 's/^/nopf /' >> gpurun_out/mlp_pf.log 2>&1 || exit 1
-done && \
-timeout -k 10 300 python -u tools/config_bench.py --only C3,C4-full,C5 --frames 5 > gpurun_out/cfg_pf.log 2>&1 && \
-NR_LIBRARY=$ALT timeout -k 10 300 python -u tools/config_bench.py --only C3,C4-full --frames 5 | sed 's/^/nopf /' >> gpurun_out/cfg_pf.log 2>&1
+L=gpurun_out/pf2.log
+ab() {
+  echo "== $1" >> $L
+  NR_LIBRARY=$2 timeout -k 10 120 python -u tools/mlp_latency.py >> $L 2>&1 &&
+  NR_LIBRARY=$2 timeout -k 10 200 python -u tools/batch_bench.py --frames 64 --batches 1,20 --shards 1,8 >> $L 2>&1
+}
+ab prefetch $PWD/cudaneuralrender_amd/lib/libnr.so &&
+ab prev $PWD/build/prev/libnr.so &&
+ab prefetch-again $PWD/cudaneuralrender_amd/lib/libnr.so &&
+ab prev-again $PWD/build/prev/libnr.so
