@@ -309,6 +309,22 @@ int num_cus(int dev) {
 
 int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
 
+// Block-cost buffers of the temporal order / cost probe for a frame-shard shape: a new shape
+// (key) invalidates the recorded order; the buffers grow with the block count.
+int order_buffers(nr_ctx *c, int W, int H, int band, int nshards, int shard, int nblocks) {
+    const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
+    if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
+    if ((size_t)nblocks > c->cap_blocks) {
+        dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
+        HIPCHK(c, hipMalloc(&c->d_bcost, (size_t)nblocks * 4));
+        HIPCHK(c, hipMalloc(&c->d_order[0], (size_t)nblocks * 4));
+        HIPCHK(c, hipMalloc(&c->d_order[1], (size_t)nblocks * 4));
+        c->cap_blocks = nblocks;
+        c->order_valid = 0;
+    }
+    return NR_OK;
+}
+
 // Per-frame arguments of a batch: pinned staging (reused only once the previous upload
 // has been consumed) + device copy.  With host outputs the frames of one launch go
 // through d_bout (`chunk` frames).
@@ -864,6 +880,13 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     T.take = c->wave_rays;
     T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
     const int cus = num_cus(c->device);
+    // temporal block order (nr_set_temporal_order): every launch dispenses the blocks of its
+    // frames longest-first by the costs the previous launch of this frame-shard shape recorded
+    // (the block layout is the same for every frame of a batch; the costs are the max over them)
+    if (c->temporal) {
+        int rc3;
+        if ((rc3 = order_buffers(c, W, H, band, nshards, shard, T.nblocks)) != NR_OK) return rc3;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, s));
     int launches = 0;
     for (int f0 = 0; f0 < nframes; f0 += chunk) {
@@ -890,10 +913,20 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
                         : (c->precision == NR_PRECISION_FP32 && npix * n >= ((size_t)8 << 20)) ? 4 : 3;
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
+        if (c->temporal) {
+            T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
+            T.bcost = c->d_bcost;
+            HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
+        }
         int rc2;
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
         HIPCHK(c, launch_trace(A, mlp_for_frames(c, frames, nframes, 0), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
+        if (c->temporal) {  // the order for the next launch of this shape
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, 0, s));
+            c->order_cur ^= 1;
+            c->order_valid = 1;
+        }
         ++launches;
         if (loc != NR_DEVICE)
             for (int i = f0; i < f0 + n; ++i)
@@ -1007,19 +1040,9 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.inv_band = 1.0 / (double)band;
         T.take = c->wave_rays;
         T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
-        const long long key = ((((long long)W * 65536 + H) * 4096 + band) * 64 + nshards) * 64 + shard;
-        if (key != c->order_key) { c->order_valid = 0; c->order_key = key; }
+        if (c->temporal || c->probe_steps > 0)
+            if ((rc2 = order_buffers(c, W, H, band, nshards, shard, T.nblocks)) != NR_OK) return rc2;
         const bool probe = c->probe_steps > 0 && max_steps > 0 && !(c->temporal && c->order_valid);
-        if (c->temporal || probe) {
-            if ((size_t)T.nblocks > c->cap_blocks) {
-                dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]);
-                HIPCHK(c, hipMalloc(&c->d_bcost, (size_t)T.nblocks * 4));
-                HIPCHK(c, hipMalloc(&c->d_order[0], (size_t)T.nblocks * 4));
-                HIPCHK(c, hipMalloc(&c->d_order[1], (size_t)T.nblocks * 4));
-                c->cap_blocks = T.nblocks;
-                c->order_valid = 0;
-            }
-        }
         if (c->temporal) {
             T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
             T.bcost = c->d_bcost;

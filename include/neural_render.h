@@ -202,9 +202,10 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * A/B of the two forms).  Bit 10 = nr_render_batch deals its pixel queue frame after
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
 int nr_set_debug(nr_ctx *ctx, int flags);
-/* Temporal scheduling: each frame records its 8x8 pixel blocks' longest ray and the
- * next frame of the same size/shard dispenses blocks longest-first (pixels are
- * unaffected -- only the order work is handed out changes). */
+/* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
+ * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next
+ * launch of the same size/shard dispenses blocks longest-first (pixels are unaffected --
+ * only the order work is handed out changes). */
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);

@@ -250,6 +250,30 @@ def test_temporal_order_same_pixels(rend, nets, chrome, W, H):
     assert sa["ray_steps"] == sb["ray_steps"] == sc["ray_steps"]
 
 
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_temporal_order_batch_same_pixels(rend, nets, chrome, prec):
+    """nr_render_batch with the temporal order: the first batch records its block costs, the
+    next (and a sharded one after it, whose shape invalidates the order) hand the blocks out
+    longest-first; pixels and ray-steps equal the plain batch."""
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec)
+    rend.set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    cams = [(*nr.camera(-20.0 + 10 * i, 40.0 * i, 2.0), i) for i in range(5)]
+    try:
+        a, sa = rend.render_batch(160, 120, cams, 128)
+        rend.set_temporal_order(True)
+        b, sb = rend.render_batch(160, 120, cams, 128)
+        c, sc = rend.render_batch(160, 120, cams, 128)
+        d, sd = rend.render_batch(160, 120, cams, 128, band=1, nshards=3, shard=1)
+        rend.set_temporal_order(False)
+        e, se = rend.render_batch(160, 120, cams, 128, band=1, nshards=3, shard=1)
+        assert all(np.array_equal(x, y) and np.array_equal(x, z) for x, y, z in zip(a, b, c))
+        assert sa["ray_steps"] == sb["ray_steps"] == sc["ray_steps"]
+        assert all(np.array_equal(x, y) for x, y in zip(d, e)) and sd["ray_steps"] == se["ray_steps"]
+    finally:
+        rend.set_temporal_order(False).set_precision("fp32")
+
+
 def test_render_deterministic(rend, nets, chrome):
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision("fp32")
