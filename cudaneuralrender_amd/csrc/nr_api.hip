@@ -907,10 +907,13 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // and a 4th once a launch holds >= 8 M fp32 pixels (the 38 KB fp32 workgroup fits 4 to a
         // CU since r2: 1024^2 x 32 frames 1.902 -> 1.866 ms/frame; one 8-way shard x 8 frames,
         // 1 M pixels, 0.366 -> 0.410, profiles/r2_occupancy.txt).  bf16/fp16 waves need 150
-        // VGPRs: 3 per SIMD at most.
+        // VGPRs: 3 per SIMD at most.  An fp32 launch of under 1 M pixels (e.g. one 8-way shard
+        // x 4 frames) keeps 2: its tail outweighs the bulk (0.420 -> 0.385 ms/frame,
+        // profiles/r2_single_bpc.txt).
+        const bool fp32 = c->precision == NR_PRECISION_FP32;
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu
-                        : n < 4 ? 2
-                        : (c->precision == NR_PRECISION_FP32 && npix * n >= ((size_t)8 << 20)) ? 4 : 3;
+                        : (n < 4 || (fp32 && npix * n < ((size_t)1 << 20))) ? 2
+                        : (fp32 && npix * n >= ((size_t)8 << 20)) ? 4 : 3;
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         if (c->temporal) {
