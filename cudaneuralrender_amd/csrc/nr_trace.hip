@@ -477,12 +477,16 @@ __global__ __launch_bounds__(256, (PREC == NR_PRECISION_FP32 && BATCH) ? NR_TRAC
     }
 }
 
+// waves per SIMD k_mlp16's registers target (<= 96 VGPRs at 5)
+#ifndef NR_MLP16_WPS
+#define NR_MLP16_WPS 5
+#endif
 // Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
 // matrix-core tiles: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks; the next
 // chunk's inputs are loaded before the current chunk's MLP, so their HBM latency (~2 us)
 // hides behind its MFMAs instead of stalling every wave once per chunk.
 template <int PREC>
-__global__ __launch_bounds__(256, 2) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
+__global__ __launch_bounds__(256, NR_MLP16_WPS) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     // the wave's chunk index is uniform: readfirstlane keeps the loop control (base, rem,
