@@ -309,6 +309,23 @@ int num_cus(int dev) {
 
 int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
 
+// Persistent-tracer workgroups per CU for a launch of `total` pixels over `nframes` frames
+// (profiles/r2_occupancy.txt, r2_single_bpc.txt, r2_lowp_occ.txt):
+//   fp32: 2 for one frame or fewer than 4 frames or under 1 M pixels (the tail outweighs the
+//         bulk), 4 from 8 M pixels (the 38 KB, <= 128-VGPR batched instance), else 3;
+//   bf16/fp16 (<= 128 VGPRs, 31 KB): 2 under 1 M pixels, 3 under 2 M (a 1024^2 frame: 0.885 /
+//         0.843 / 0.856 ms at 2 / 3 / 4), else 4 (1024^2 x 20: 0.424 -> 0.404 ms/frame at 3 -> 4,
+//         2048^2 x 8: 1.661 -> 1.569, one 2048^2 frame 2.503 -> 2.481).
+int default_bpc(const nr_ctx *c, size_t total, int nframes) {
+    const size_t M = (size_t)1 << 20;
+    if (c->precision == NR_PRECISION_FP32) {
+        if (nframes < 4 || total < M) return 2;
+        return total >= 8 * M ? 4 : 3;
+    }
+    if (total < M) return 2;
+    return total < 2 * M ? 3 : 4;
+}
+
 // Block-cost buffers of the temporal order / cost probe for a frame-shard shape: a new shape
 // (key) invalidates the recorded order; the buffers grow with the block count.
 int order_buffers(nr_ctx *c, int W, int H, int band, int nshards, int shard, int nblocks) {
@@ -901,19 +918,9 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         T.interleave = !((c->debug >> 10) & 1);
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
-        // 3 workgroups (12 waves) per CU once several frames share the launch: the third
-        // wave per SIMD lifts the bulk rate, and the frames' tails overlap instead of
-        // adding up (tools/batch_bench.py); a lone frame keeps the single-frame default
-        // and a 4th once a launch holds >= 8 M fp32 pixels (the 38 KB fp32 workgroup fits 4 to a
-        // CU since r2: 1024^2 x 32 frames 1.902 -> 1.866 ms/frame; one 8-way shard x 8 frames,
-        // 1 M pixels, 0.366 -> 0.410, profiles/r2_occupancy.txt).  bf16/fp16 waves need 150
-        // VGPRs: 3 per SIMD at most.  An fp32 launch of under 1 M pixels (e.g. one 8-way shard
-        // x 4 frames) keeps 2: its tail outweighs the bulk (0.420 -> 0.385 ms/frame,
-        // profiles/r2_single_bpc.txt).
-        const bool fp32 = c->precision == NR_PRECISION_FP32;
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu
-                        : (n < 4 || (fp32 && npix * n < ((size_t)1 << 20))) ? 2
-                        : (fp32 && npix * n >= ((size_t)8 << 20)) ? 4 : 3;
+        // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,
+        // so the extra waves per SIMD lift the bulk rate instead of lengthening the tail)
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix * n, n);
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         if (c->temporal) {
@@ -1050,7 +1057,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
             T.bcost = c->d_bcost;
         }
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 2;
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix, 1);
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         if (c->debug & 1) {

@@ -27,9 +27,12 @@ namespace nr {
 #ifndef NR_TRACE_BPC
 #define NR_TRACE_BPC 3
 #endif
-// the batched fp32 instance: 4 workgroups per CU (<= 128 VGPRs) for launches of >= 8 M pixels
-#ifndef NR_TRACE_BPC_F32_BATCH
-#define NR_TRACE_BPC_F32_BATCH 4
+// the batched fp32 instance and the reduced-precision ones: 4 workgroups per CU (<= 128 VGPRs,
+// a few values spilled outside the MLP) -- fp32 launches of >= 8 M pixels run 4 (1024^2 x 20
+// frames 1.795 -> 1.772 ms/frame), bf16 launches too (0.416 -> 0.408 ms/frame, C3 batch 1.660 ->
+// 1.632; profiles/r2_f32_batch_bounds.txt, r2_lowp_bpc4.txt)
+#ifndef NR_TRACE_BPC_WIDE
+#define NR_TRACE_BPC_WIDE 4
 #endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
@@ -141,7 +144,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // frame-dependent values (camera, sphere offset, animation input, output image) come
 // from the FrameArgs staged in LDS.
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
-__global__ __launch_bounds__(256, (PREC == NR_PRECISION_FP32 && BATCH) ? NR_TRACE_BPC_F32_BATCH : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, (PREC != NR_PRECISION_FP32 || BATCH) ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
