@@ -411,34 +411,34 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
-    const uint32_t hm = 0u - (uint32_t)h;  // all ones in the upper half
     f32x16 acc[NT];
     {
-        float xv[2], yv[2], zv[2], fv[2];
-        half_views(x, xv[0], xv[1]);
-        half_views(y, yv[0], yv[1]);
-        half_views(z, zv[0], zv[1]);
-        if (in0 == 4) half_views(fr, fv[0], fv[1]);
-        else fv[0] = fv[1] = 0.0f;
+        // B operand of tile t, lanes 0-31 (k 0-7) of point l: {xh, yh | zh, xl | yl, zl | fh, fl};
+        // lanes 32-63 (k 8-15) of point l - 32: {xh, yh | zh, fh | 0 | 0}.  Each lane splits
+        // its own point once (the residuals x - xh are exact in f32) and v_permlane32_swap(a, b)
+        // = {[a lanes 0-31 | b lanes 0-31], [a lanes 32-63 | b lanes 32-63]} deals the packed
+        // words to both tiles: word 1 swaps {zh, xl} against {zh, fh}, words 2-3 against 0.
+        // (Round 2 split both tiles' points in every lane and assembled them with bit
+        // selects: the same operands, ~20 more VALU per 64 points.)
+        const uint32_t p0 = cvt2<PREC>(x, y);                                   // xh, yh
+        const float dx = x - lo16f<PREC>(p0), dy = y - hi16f<PREC>(p0);
+        const uint32_t q = cvt2<PREC>(z, dx);                                    // zh, xl
+        const uint32_t r = cvt2<PREC>(dy, z - lo16f<PREC>(q));                   // yl, zl
+        uint32_t f = 0;                                                          // fh, fl
+        if (in0 == 4) {
+            const uint32_t f0 = cvt2<PREC>(fr, 0.0f);
+            f = cvt2<PREC>(fr, fr - lo16f<PREC>(f0));
+        }
+        const uint32_t qf = (q & 0xffffu) | (f << 16);                           // zh, fh
+        const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
+        const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
+        const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
+        const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
         const v8 A = reinterpret_cast<const v8 *>(lp)[lane];
         const f32x16 b0 = load_bias16(fl + 16 * h);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            // B operand, h = 0: {xh, yh | zh, xl | yl, zl | fh, fl}; h = 1: {xh, yh | zh, fh | 0 | 0}
-            // (the residuals x - xh are exact in f32; bit selects, so that nothing is computed
-            // under a lane-dependent branch)
-            const uint32_t p0 = cvt2<PREC>(xv[t], yv[t]);                             // xh, yh
-            const float dx = xv[t] - lo16f<PREC>(p0), dy = yv[t] - hi16f<PREC>(p0);
-            const uint32_t q = cvt2<PREC>(zv[t], dx);                                  // zh, xl
-            const uint32_t r = cvt2<PREC>(dy, zv[t] - lo16f<PREC>(q));                 // yl, zl
-            uint32_t f = 0;                                                            // fh, fl
-            if (in0 == 4) {
-                const uint32_t f0 = cvt2<PREC>(fv[t], 0.0f);
-                f = cvt2<PREC>(fv[t], fv[t] - lo16f<PREC>(f0));
-            }
-            const uint32_t w1 = (q & ~hm) | (((q & 0xffffu) | (f << 16)) & hm);
-            acc[t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){p0, w1, r & ~hm, f & ~hm}), b0);
-        }
+        for (int t = 0; t < NT; ++t)
+            acc[t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){w0[t], w1[t], w2[t], w3[t]}), b0);
     }
     hidden_layers<PREC, NT, NH, CL>(lp, fl, nh, acc);
     // final 32 -> 1 layer on the VALU: lane l holds 16 of point (l & 31)'s units as the 8
