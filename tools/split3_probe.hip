@@ -50,7 +50,7 @@ __host__ __device__ inline int col_of(int s, int h, int i) { return row_of(8 * s
 // MODE 0: one f16 term; 1: f16 three-term split; 2: bf16 three-term split; 3: one bf16 term
 template <int MODE>
 __global__ __launch_bounds__(256, 4) void k_probe(const uint4 *__restrict__ Ah, const uint4 *__restrict__ Al,
-                                                  const float *__restrict__ bias, float *__restrict__ out, long n) {
+                                                  const float *__restrict__ bias, float *__restrict__ out, long n, int nl) {
     constexpr bool BF = MODE >= 2;
     typedef typename std::conditional<BF, bf16x8, f16x8>::type v8;
     typedef typename std::conditional<BF, __bf16, _Float16>::type e16;
@@ -65,7 +65,8 @@ __global__ __launch_bounds__(256, 4) void k_probe(const uint4 *__restrict__ Ah, 
             for (int r = 0; r < 16; ++r) acc[t][r] = input_of(p, row_of(r, h));
         }
 #pragma unroll 1
-        for (int l = 0; l < NL; ++l) {
+        for (int ll = 0; ll < nl; ++ll) {
+            const int l = ll % NL;  // nl > NL repeats the layers: the marginal cost of a layer
             v8 wh[2], wl[2];
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256, 4) void k_probe(const uint4 *__restrict__ Ah, 
                 for (int s = 0; s < 2; ++s)
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
-                        const float a = l == 0 ? acc[t][8 * s + i] : fmaxf(acc[t][8 * s + i], 0.0f);
+                        const float a = ll == 0 ? acc[t][8 * s + i] : fmaxf(acc[t][8 * s + i], 0.0f);
                         const e16 hi = (e16)a;
                         xh[s][i] = hi;
                         if (MODE == 1 || MODE == 2) xl[s][i] = (e16)(a - (float)hi);
@@ -226,26 +227,31 @@ int main(int argc, char **argv) {
     std::vector<float> out(ncheck);
     for (int mode = 0; mode < 4; ++mode) {
         const int f = mode >= 2 ? 1 : 0;
-        auto launch = [&]() {
-            if (mode == 0) hipLaunchKernelGGL(k_probe<0>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n);
-            if (mode == 1) hipLaunchKernelGGL(k_probe<1>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n);
-            if (mode == 2) hipLaunchKernelGGL(k_probe<2>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n);
-            if (mode == 3) hipLaunchKernelGGL(k_probe<3>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n);
+        auto launch = [&](int nl) {
+            if (mode == 0) hipLaunchKernelGGL(k_probe<0>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
+            if (mode == 1) hipLaunchKernelGGL(k_probe<1>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
+            if (mode == 2) hipLaunchKernelGGL(k_probe<2>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
+            if (mode == 3) hipLaunchKernelGGL(k_probe<3>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
         };
-        launch();
-        CHECK(hipDeviceSynchronize());
-        CHECK(hipEventRecord(e0));
-        for (int r = 0; r < reps; ++r) launch();
-        CHECK(hipEventRecord(e1));
-        CHECK(hipEventSynchronize(e1));
-        float ms;
-        CHECK(hipEventElapsedTime(&ms, e0, e1));
-        ms /= reps;
+        float ms2 = 0.0f, ms = 0.0f;
+        for (int nl : {2 * NL, NL}) {  // the last pass (NL layers) is the one checked
+            launch(nl);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(e0));
+            for (int r = 0; r < reps; ++r) launch(nl);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            if (nl == 2 * NL) { ms2 = ms; continue; }
+        }
         CHECK(hipMemcpy(out.data(), dOut, ncheck * 4, hipMemcpyDeviceToHost));
         double err = 0;
         for (int p = 0; p < ncheck; ++p) err = std::max(err, std::fabs((double)out[p] - ref[p]));
         const double tf = (double)n * NL * 2 * 32 * 32 / (ms * 1e-3) / 1e12;
-        printf("%-14s %8.4f ms  %7.1f TFLOP/s (hidden-layer FLOP)  max abs err vs fp64 %.3e\n", names[mode], ms, tf, err);
+        const double tfm = (double)n * NL * 2 * 32 * 32 / ((ms2 - ms) * 1e-3) / 1e12;
+        printf("%-14s %8.4f ms  %7.1f TFLOP/s (hidden-layer FLOP)  max abs err vs fp64 %.3e;  %d layers %.4f ms: marginal %.1f TFLOP/s per added layer\n",
+               names[mode], ms, tf, err, 2 * NL, ms2, tfm);
     }
     return 0;
 }
