@@ -120,6 +120,87 @@ __global__ __launch_bounds__(256, 4) void k_probe(const uint4 *__restrict__ Ah, 
     }
 }
 
+// A tuned f16 variant (closer to k_mlp16's code shape): A operands and the D-layout biases
+// staged in LDS, NLT layers (repeating the NL weight sets; unrolling them spills the hoisted weights),
+// packed conversions (v_cvt_pk_f16_f32 pairs; the split's residual from the unpacked high
+// halves).  SPLIT: the three-term split; otherwise one f16 term.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <bool SPLIT, int NLT>
+__global__ __launch_bounds__(256, 4) void k_tuned(const uint4 *__restrict__ Ah, const uint4 *__restrict__ Al,
+                                                  const float *__restrict__ biasD, float *__restrict__ out, long n) {
+    __shared__ uint4 sAh[NL * 2 * 64], sAl[NL * 2 * 64];
+    __shared__ f32x16 sB[NL * 2];
+    for (int i = threadIdx.x; i < NL * 2 * 64; i += blockDim.x) {
+        sAh[i] = Ah[i];
+        if (SPLIT) sAl[i] = Al[i];
+    }
+    for (int i = threadIdx.x; i < NL * 2 * 16; i += blockDim.x) reinterpret_cast<float *>(sB)[i] = biasD[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, h = lane >> 5;
+    const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+    for (long c = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c * 64 < n; c += nw) {
+        f32x16 acc[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint32_t p = (uint32_t)(c * 64 + 32 * t + (lane & 31));
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[t][r] = input_of(p, row_of(r, h));
+        }
+#pragma unroll 1
+        for (int ll = 0; ll < NLT; ++ll) {
+            const int l = ll % NL;
+            f16x8 wh[2], wl[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                wh[s] = __builtin_bit_cast(f16x8, sAh[(l * 2 + s) * 64 + lane]);
+                if (SPLIT) wl[s] = __builtin_bit_cast(f16x8, sAl[(l * 2 + s) * 64 + lane]);
+            }
+            const f32x16 b = sB[l * 2 + h];
+            f16x8 xh[2][2], xl[2][2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    u32x4 hw, lw;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        f32x2 v = {acc[t][8 * s + 2 * q], acc[t][8 * s + 2 * q + 1]};
+                        if (ll > 0) v = __builtin_elementwise_max(v, (f32x2){0.0f, 0.0f});
+                        const f16x2 hi = __builtin_convertvector(v, f16x2);
+                        hw[q] = __builtin_bit_cast(uint32_t, hi);
+                        if (SPLIT) lw[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v - __builtin_convertvector(hi, f32x2), f16x2));
+                    }
+                    xh[t][s] = __builtin_bit_cast(f16x8, hw);
+                    if (SPLIT) xl[t][s] = __builtin_bit_cast(f16x8, lw);
+                }
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                f32x16 d = b;
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    d = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[s], xh[t][s], d, 0, 0, 0);
+                    if (SPLIT) {
+                        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[s], xl[t][s], d, 0, 0, 0);
+                        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[s], xh[t][s], d, 0, 0, 0);
+                    }
+                }
+                acc[t] = d;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            float sum = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sum += fmaxf(acc[t][r], 0.0f);
+            sum += __shfl_xor(sum, 32);
+            const long p = c * 64 + 32 * t + (lane & 31);
+            if (h == 0 && p < n) out[p] = sum;
+        }
+    }
+}
+
 static uint16_t f16_bits(float v) {
     _Float16 x = (_Float16)v;
     uint16_t b;
@@ -214,6 +295,13 @@ int main(int argc, char **argv) {
         CHECK(hipMemcpy(dAh[f], ah[f].data(), ah[f].size() * 2, hipMemcpyHostToDevice));
         CHECK(hipMemcpy(dAl[f], al[f].data(), al[f].size() * 2, hipMemcpyHostToDevice));
     }
+    std::vector<float> BD(NL * 2 * 16);  // biases in the D layout: [layer][half][register]
+    for (int l = 0; l < NL; ++l)
+        for (int hh = 0; hh < 2; ++hh)
+            for (int r = 0; r < 16; ++r) BD[(l * 2 + hh) * 16 + r] = B[l * 32 + row_of(r, hh)];
+    float *dBD;
+    CHECK(hipMalloc(&dBD, BD.size() * 4));
+    CHECK(hipMemcpy(dBD, BD.data(), BD.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMalloc(&dB, B.size() * 4));
     CHECK(hipMemcpy(dB, B.data(), B.size() * 4, hipMemcpyHostToDevice));
     CHECK(hipMalloc(&dOut, n * 4));
@@ -223,15 +311,19 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const char *names[4] = {"f16 x1", "f16 x3 split", "bf16 x3 split", "bf16 x1"};
+    const char *names[6] = {"f16 x1", "f16 x3 split", "bf16 x3 split", "bf16 x1", "f16 x1 tuned", "f16 x3 tuned"};
     std::vector<float> out(ncheck);
-    for (int mode = 0; mode < 4; ++mode) {
-        const int f = mode >= 2 ? 1 : 0;
+    for (int mode = 0; mode < 6; ++mode) {
+        const int f = (mode == 2 || mode == 3) ? 1 : 0;
         auto launch = [&](int nl) {
             if (mode == 0) hipLaunchKernelGGL(k_probe<0>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
             if (mode == 1) hipLaunchKernelGGL(k_probe<1>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
             if (mode == 2) hipLaunchKernelGGL(k_probe<2>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
             if (mode == 3) hipLaunchKernelGGL(k_probe<3>, dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dB, dOut, n, nl);
+            if (mode == 4 && nl == NL) hipLaunchKernelGGL((k_tuned<false, NL>), dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dBD, dOut, n);
+            if (mode == 4 && nl != NL) hipLaunchKernelGGL((k_tuned<false, 2 * NL>), dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dBD, dOut, n);
+            if (mode == 5 && nl == NL) hipLaunchKernelGGL((k_tuned<true, NL>), dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dBD, dOut, n);
+            if (mode == 5 && nl != NL) hipLaunchKernelGGL((k_tuned<true, 2 * NL>), dim3(grid), dim3(256), 0, 0, dAh[f], dAl[f], dBD, dOut, n);
         };
         float ms2 = 0.0f, ms = 0.0f;
         for (int nl : {2 * NL, NL}) {  // the last pass (NL layers) is the one checked
