@@ -30,6 +30,13 @@ is checked against a reference render afterwards (config.parity_frames_checked).
 config.random_poses repeats the timing over 8 poses from default_rng(1) (rx in [-30, 30],
 ry in [0, 360), zoom 2), the K frames cycling through them.
 
+--config c3 / c4 / c5 time the other BASELINE configs with the same harness (c3 car_1 2048^2
+bf16 256 steps; c4 plane_2 4096^2 bf16, row-band shards + gather; c5 one geometry per rank,
+GEOMS[rank % 5], 2048^2 fp16, independent replicas with no collective: scaling "weak",
+config.per_rank_value).  With fp32, config.fp32x3 times the same K frames in
+NR_PRECISION_FP32X3 (the fp32-class split on the fp16 matrix core; its pixel contract is
+tests/test_gpu_fp32x3.py) and reports its agreement with the fp32 frame.
+
 Prints ONE JSON line on rank 0 (driver contract) with `roofline` (dominant kernel
 k_trace, f32 MFMA bound, per-launch HIP events on the stream it runs on; per rank for
 N > 1) and `cpu_baseline` (the C oracle on the host cores, N = 1 only: all-core value
@@ -49,7 +56,18 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 FLOP_PER_EVAL = 2 * (3 * 32 + 7 * 32 * 32 + 32 * 1)   # 14,592
-PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}  # TFLOP/s dense, MI355X_MICROARCH.md
+# TFLOP/s dense, MI355X_MICROARCH.md; fp32x3 runs its hidden layers as three fp16 MFMA terms, so
+# its roofline is the fp16 matrix peak (achieved counts the algorithmic 14,592 FLOP per eval)
+PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6, "fp32x3": 2516.6}
+GEOMS = ["plane_1", "plane_2", "plane_3", "car_1", "3a3d4a90a2db90b4203936772104a82d.obj"]
+# BASELINE.json configs: c2 is the headline (configs[1]); c3 / c4 / c5 are configs[2..4].
+# c5 renders one geometry per rank (GEOMS[rank % 5]) as independent replicas: no collective.
+PRESETS = {
+    "c2": dict(geometry="plane_1", size=1024, precision="fp32", max_steps=128),
+    "c3": dict(geometry="car_1", size=2048, precision="bf16", max_steps=256),
+    "c4": dict(geometry="plane_2", size=4096, precision="bf16", max_steps=128),
+    "c5": dict(geometry=None, size=2048, precision="fp16", max_steps=128),
+}
 MAX_STEPS = 128
 BAND = 1  # rows per band dealt round-robin to the ranks (profiles/r1_shard_balance.txt)
 MAX_BATCH = 32  # frames per k_trace launch (NR_MAX_BATCH)
@@ -60,16 +78,25 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
-    ap.add_argument("--size", type=int, default=1024)
-    ap.add_argument("--max-steps", type=int, default=MAX_STEPS)
-    ap.add_argument("--geometry", default="plane_1")
+    ap.add_argument("--config", default="c2", choices=sorted(PRESETS),
+                    help="BASELINE config preset (c2 = the headline); the flags below override it")
+    ap.add_argument("--precision", default=None, choices=["fp32", "bf16", "fp16", "fp32x3"])
+    ap.add_argument("--size", type=int, default=None)
+    ap.add_argument("--max-steps", type=int, default=None)
+    ap.add_argument("--geometry", default=None)
+    ap.add_argument("--no-fp32x3", action="store_true",
+                    help="skip config.fp32x3 (the same frames timed in NR_PRECISION_FP32X3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-frame", action="store_true")
     ap.add_argument("--no-random-poses", action="store_true",
                     help="skip config.random_poses (profiling passes that average the default-pose launches)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    a.replicas = a.config == "c5"
+    return a
 
 
 def cpu_model():
@@ -157,26 +184,29 @@ def main():
     size = a.size
     matcap = nr.load_png(nr.matcap_path("Chrome"))
     iv, nm = nr.camera(0.0, 0.0, 2.0)
-    rows = nr.shard_rows(size, BAND, world, rank)
-    max_rows = max(nr.shard_rows(size, BAND, world, s) for s in range(world))
+    # replicas (c5): every rank renders whole frames of its own geometry, no shards, no collective
+    nsh, sh = (1, 0) if a.replicas else (world, rank)
+    geometry = a.geometry or GEOMS[rank % len(GEOMS)]
+    max_rows = max(nr.shard_rows(size, BAND, nsh, s) for s in range(nsh))
 
     stream = torch.cuda.Stream()
     r = nr.Renderer(local)
-    r.load_h5(nr.geometry_path(a.geometry)).set_precision(a.precision)
+    r.load_h5(nr.geometry_path(geometry)).set_precision(a.precision)
     r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
     r.set_stream(stream.cuda_stream)
 
     nbuf = max(a.steps, a.warmup, 1)
     shard_px = max_rows * size
     shards = torch.zeros(nbuf, shard_px, dtype=torch.int32, device="cuda")
-    frames = shards if world == 1 else (
+    frames = shards if (world == 1 or a.replicas) else (
         torch.zeros(nbuf, size * size, dtype=torch.int32, device="cuda") if rank == 0 else None)
-    gather = torch.zeros(world, nbuf * shard_px, dtype=torch.int32, device="cuda") if (rank == 0 and world > 1) else None
+    gather = (torch.zeros(world, nbuf * shard_px, dtype=torch.int32, device="cuda")
+              if (rank == 0 and world > 1 and not a.replicas) else None)
 
     def collect(i0, n):
         """Frames i0..i0+n-1 to rank 0: ONE RCCL gather of the n shards of every rank, then
         the re-interleave kernel per frame (rank s's shard of frame i at gather[s][i])."""
-        if world == 1:
+        if world == 1 or a.replicas:
             return
         src = shards[i0:i0 + n].reshape(-1)
         dist.gather(src, [g[: n * shard_px] for g in gather.unbind(0)] if rank == 0 else None, dst=0)
@@ -203,7 +233,7 @@ def main():
             return
         with torch.cuda.stream(stream):
             st = r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size,
-                                       [cams[i % len(cams)] for i in range(n)], a.max_steps, BAND, world, rank,
+                                       [cams[i % len(cams)] for i in range(n)], a.max_steps, BAND, nsh, sh,
                                        with_stats=True)
             counted["ray_steps"] += st["ray_steps"]
             counted["shade_evals"] += st["shade_evals"]
@@ -212,7 +242,7 @@ def main():
     def run_single(n):
         with torch.cuda.stream(stream):
             for i in range(n):
-                st = r.render_shard_device(shards[i].data_ptr(), size, size, BAND, world, rank, a.max_steps,
+                st = r.render_shard_device(shards[i].data_ptr(), size, size, BAND, nsh, sh, a.max_steps,
                                            with_stats=True)
                 counted["ray_steps"] += st["ray_steps"]
                 counted["shade_evals"] += st["shade_evals"]
@@ -279,6 +309,28 @@ def main():
         dt_pose, _, rs_pose, se_pose, _ = timed(lambda n: run_batched(n, pose_cams), False)
         pose_parity, pose_checked = check_frames(a.steps, pose_cams)
 
+    # the same K frames in NR_PRECISION_FP32X3 (fp32-class MLP on the fp16 matrix core, not
+    # bit-exact: tests/test_gpu_fp32x3.py holds its pixel contract), next to the fp32 headline
+    x3 = None
+    if a.precision == "fp32" and not a.no_fp32x3:
+        ref = None
+        if rank == 0:
+            img = r.render(size, size, a.max_steps, with_stats=False)
+            ref = torch.from_numpy(img.view(np.int32).reshape(-1)).to("cuda")
+        r.set_precision("fp32x3")
+        dt3, prof3, rs3, se3, pr3 = timed(run_batched, True)
+        l3 = max(prof3["march_launches"], 1)
+        ms3 = prof3["march_ms"] / l3
+        ach3 = float(pr3[rank, 1] + pr3[rank, 2]) * FLOP_PER_EVAL / l3 / (ms3 * 1e-3) / 1e12 if ms3 > 0 else 0.0
+        x3 = {"value": round(rs3 / dt3 / 1e6, 3), "ms_per_step": round(dt3 / a.steps * 1e3, 4),
+              "fps": round(a.steps / dt3, 3), "ray_steps_per_frame": int(rs3 / a.steps),
+              "k_trace_avg_launch_ms": round(ms3, 5),
+              "roofline_frac_fp16_peak": round(ach3 / PEAK["fp32x3"], 4),
+              "achieved_TFLOPs_algorithmic": round(ach3, 3)}
+        if rank == 0:
+            x3["identical_pixels_vs_fp32"] = round(float((frames[0][: size * size] == ref).float().mean()), 5)
+        r.set_precision(a.precision)
+
     # roofline of the dominant kernel (k_trace) from this rank's per-launch events
     launches = max(prof["march_launches"], 1)
     march_avg_ms = prof["march_ms"] / launches
@@ -304,7 +356,7 @@ def main():
             tp = json.load(open(os.path.join(REPO, "profiles", name)))
         except (OSError, ValueError):
             continue
-        if a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1:
+        if a.config == "c2" and a.precision == "fp32" and size == 1024 and a.max_steps == 128 and world == 1:
             per_frame = tp.get("hbm_bytes_per_frame")
             if per_frame is None and tp.get("frames_per_launch"):
                 per_frame = tp["hbm_bytes_per_launch"] / tp["frames_per_launch"]
@@ -319,7 +371,8 @@ def main():
         return
     value = ray_steps_k / dt / 1e6
     out = {
-        "metric": "Mray-steps/s at 1024^2, plane_1.h5 (frames/s in config.fps)",
+        "metric": "Mray-steps/s at 1024^2, plane_1.h5 (frames/s in config.fps)" if a.config == "c2" else
+                  f"Mray-steps/s, BASELINE {a.config} (frames/s in config.fps)",
         "value": round(value, 3),
         "unit": "Mray-steps/s",
         "n_gpus": world,
@@ -327,13 +380,16 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(dt / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if a.replicas else "strong",
         "vs_baseline": None,
         "dtype": "f32" if a.precision == "fp32" else a.precision,
-        "data": "synthetic camera (default pose), real bundled weights plane_1.h5 + Chrome.png",
+        "data": f"synthetic camera (default pose), real bundled weights {geometry}.h5 + Chrome.png"
+                if not a.replicas else "synthetic camera (default pose), rank r renders bundled geometry r % 5",
         "config": {
-            "workload": f"{a.geometry} {size}x{size}, {a.max_steps} march steps, {a.precision}, Chrome.png, "
-                        "v1 scene, default camera (BASELINE configs[1])",
+            "workload": (f"{geometry if not a.replicas else 'GEOMS[rank % 5]'} {size}x{size}, {a.max_steps} march "
+                         f"steps, {a.precision}, Chrome.png, v1 scene, default camera (BASELINE "
+                         f"configs[{ {'c2': 1, 'c3': 2, 'c4': 3, 'c5': 4}[a.config] }])"),
+            "config": a.config,
             "fps": round(a.steps / dt, 3),
             "ray_steps_counted": int(ray_steps_k),
             "ray_steps_per_frame": int(ray_steps_k / a.steps),
@@ -341,8 +397,12 @@ def main():
             "frames_per_launch": min(a.steps, MAX_BATCH),
             "schedule": "nr_render_batch: the K timed frames through one pixel queue, 64-pixel chunks "
                         "dealt to the frames in turn (every frame rendered in full)",
-            "parallelism": f"row-band shards x{world} (band {BAND}) + one RCCL gather per batch of frames"
+            "parallelism": ("replicas: one geometry per rank, no collective" if a.replicas else
+                            f"row-band shards x{world} (band {BAND}) + one RCCL gather per batch of frames")
                            if world > 1 else "single GPU",
+            "per_rank_value": [round(float(x[1] / x[0] / 1e6), 3) for x in per_rank] if world > 1 else None,
+            "geometries": [GEOMS[i % len(GEOMS)] for i in range(world)] if a.replicas else None,
+            "fp32x3": x3,
             "parity_vs_single_gpu_render": parity,
             "parity_frames_checked": nchecked,
             "shard_ray_steps": {"max": int(rank_steps.max()), "mean": round(float(rank_steps.mean()), 1)}
@@ -384,7 +444,7 @@ def main():
         "cpu_baseline": None,
     }
     if world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(size, a.max_steps, a.cpu_threads, a.geometry, matcap, iv, nm)
+        out["cpu_baseline"] = cpu_baseline(size, a.max_steps, a.cpu_threads, geometry, matcap, iv, nm)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -12,7 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NR_LIBRARY") or os.path.join(_HERE, "lib", "libnr.so")
 
 NR_OK = 0
-NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2}
+NR_PRECISION = {"fp32": 0, "bf16": 1, "fp16": 2, "fp32x3": 3}
 NR_SCENE = {"v1": 0, "tanh": 1, "subtract": 2, "cylinders": 3, "displace": 4, "round": 5}
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1

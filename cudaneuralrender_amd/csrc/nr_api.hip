@@ -199,6 +199,15 @@ int upload_lowp(nr_ctx *c) {
     std::vector<uint16_t> a;
     std::vector<float> f;
     int clamp = 0;
+    if (c->precision == NR_PRECISION_FP32X3) {
+        // lp_clamp = the fp32x3 pack is valid (its scales exist); without it (or with
+        // nr_set_debug bit 9) every wave runs the fp32 MLP
+        if (!pack_x3_32(c->dims, c->kernels, c->biases, a, f, &clamp))
+            return set_err(c, NR_E_INVALID, "fp32x3 pack failed");
+        c->clamp_ok = clamp != 0;
+        c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp;
+        return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
+    }
     if (!pack_lowp_32(c->dims, c->kernels, c->biases, c->precision, a, f, &clamp))
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
     c->clamp_ok = clamp != 0;
@@ -318,6 +327,8 @@ int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
 //         2048^2 x 8: 1.661 -> 1.569, one 2048^2 frame 2.503 -> 2.481).
 int default_bpc(const nr_ctx *c, size_t total, int nframes) {
     const size_t M = (size_t)1 << 20;
+    // fp32x3: its k_trace instance is built for 3 waves per SIMD (168 VGPRs)
+    if (c->precision == NR_PRECISION_FP32X3) return total < M ? 2 : 3;
     if (c->precision == NR_PRECISION_FP32) {
         if (nframes < 4 || total < M) return 2;
         return total >= 8 * M ? 4 : 3;
@@ -770,7 +781,7 @@ int nr_mlp_info(const nr_ctx *c, int *nlayers, int *dims, int *nw, int *nb) {
 
 int nr_set_precision(nr_ctx *c, int precision) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    if (precision < NR_PRECISION_FP32 || precision > NR_PRECISION_FP16)
+    if (precision < NR_PRECISION_FP32 || precision > NR_PRECISION_FP32X3)
         return set_err(c, NR_E_INVALID, "unknown precision %d", precision);
     c->precision = precision;
     HIPCHK(c, hipSetDevice(c->device));

@@ -69,6 +69,27 @@ constexpr float LP_INPUT_BOUND = 1048576.0f;
 constexpr float F32_INPUT_BOUND = 1024.0f;
 constexpr float F32_INPUT_TINY = 0x1p-60f;
 
+// fp32x3 pack (pack_x3_32): fp32-class hidden layers on the fp16 matrix core by a three-term
+// split, a.w ~ ah.wh + al.wh + ah.wl (nr_mlp16.h mlp32_x3_nt).  16-bit elements (fp16):
+//   [0, 512)                    layer-0 A operand, as LP32 (hi/lo split of scaled weights)
+//   X3_HID + j*X3_HSTRIDE       hidden layer j: hi A operand [k-step 2][lane 64][8], then the
+//                               residual (lo) A operand in the same order (+1024)
+// floats (fl): layer-0 bias [h 2][register 16] at 0, hidden j's bias at 32 + 32j (all scaled,
+// accumulator inits), the final layer's f32 weights in the accumulator's register order
+// [h 2][register 16] at x3_final(nh), its bias at +32, then -1 (the residual's multiplier, read
+// at run time so that the compiler emits v_fma_mix), the xyz input scale and the 4th input's
+// scale.  Activations of ReLU layer l are scaled by 2^-e[l] so that their interval bound over
+// inputs within X3_INPUT_BOUND (xyz) / X3_FRAME_BOUND (4th input) is at most 2^10: the split's
+// residual (x - rtz(x)) is then below 1 and the clamp of v_fma_mixlo_f16 is its ReLU.
+constexpr int X3_HID = 512;
+constexpr int X3_HSTRIDE = 2048;
+NR_HD constexpr inline int x3_elems(int nh) { return X3_HID + nh * X3_HSTRIDE; }
+NR_HD constexpr inline int x3_final(int nh) { return 32 + 32 * nh; }
+NR_HD constexpr inline int x3_floats(int nh) { return x3_final(nh) + 36; }
+constexpr float X3_INPUT_BOUND = 4.0f;
+constexpr float X3_FRAME_BOUND = 1024.0f;
+constexpr int X3_XYZ_SHIFT = 6;  // xyz inputs enter layer 0 times 2^6
+
 bool fused_shape_ok(const std::vector<int> &dims);
 // Keras kernels (in x out, row-major) -> packs.  Return false if the shape is not
 // [3|4, 32, ..., 32, 1] (those networks render on the layered schedule).
@@ -78,6 +99,11 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
 bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, int precision,
                   std::vector<uint16_t> &a_ops, std::vector<float> &bias, int *clamp = nullptr);
+// ok (if not null) = 1 when the scales exist (every scaled weight and bound inside fp16's range);
+// otherwise the kernels run the fp32 MLP for every point
+bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
+                const std::vector<std::vector<float>> &biases, std::vector<uint16_t> &a_ops, std::vector<float> &fl,
+                int *ok = nullptr);
 
 // ---- camera (nr_camera.cpp) ----
 void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]);

@@ -616,6 +616,8 @@ hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs
         hipLaunchKernelGGL(k_march16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
     else if (prec == NR_PRECISION_FP16)
         hipLaunchKernelGGL(k_march16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (prec == NR_PRECISION_FP32X3)
+        hipLaunchKernelGGL(k_march16<NR_PRECISION_FP32X3>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
     else
         hipLaunchKernelGGL(k_march16<NR_PRECISION_FP32>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
     return hipGetLastError();

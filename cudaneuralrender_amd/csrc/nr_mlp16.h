@@ -501,11 +501,162 @@ __device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, con
     return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask);
 }
 
-// cl: see mlp16_lowp (ignored in fp32)
+// ---- fp32x3: fp32-class hidden layers on the fp16 matrix core (NR_PRECISION_FP32X3).
+// Each activation a (f32, scaled: nr_pack.cpp pack_x3_32) is split into ah = rtz_f16(a) and
+// al = rne_f16(a - ah), each weight into wh + wl (host side), and every hidden layer takes three
+// K = 32 products per tile, a.w ~ al.wh + ah.wl + ah.wh (6 v_mfma_f32_32x32x16_f16, f32
+// accumulate, the bias as the accumulator init).  The dropped al.wl and the 22-bit operands
+// leave ~2-3x the error of the f32 fmaf chain against an exact evaluation (tests/
+// test_gpu_fp32x3.py).  Per tile and layer the split is 8 v_cvt_pkrtz +
+// 8 v_pk_max_i16 (the hi words' ReLU: a negative a has a non-positive ah) + 16
+// v_fma_mix{lo,hi}_f16 with the clamp bit (the residual: a - ah has a's sign and, below 1 by the
+// pack's scaling, the clamp to [0, 1] is its ReLU) -- 32 VALU against 6 MFMAs of 32 cycles.
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+typedef short s16x2v __attribute__((ext_vector_type(2)));
+
+// accumulator registers 8s..8s+7 -> ReLU'd hi / residual B operands of k-step s.
+// m1 = -1.0f read from the pack: with a run-time multiplier the compiler forms the residual
+// as one v_fma_mix (a literal -1 folds to a subtract of the widened hi, 3 instructions)
+__device__ __forceinline__ void split_x3(const f32x16 &c, int s, float m1, f16x8 &hi, f16x8 &lo) {
+    u32x4 hw, lw;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float v0 = c[8 * s + 2 * q], v1 = c[8 * s + 2 * q + 1];
+        const f16x2v h = __builtin_bit_cast(f16x2v, __builtin_amdgcn_cvt_pkrtz(v0, v1));
+        const _Float16 l0 = __builtin_amdgcn_fmed3h((_Float16)__builtin_fmaf((float)h[0], m1, v0), (_Float16)0.0f,
+                                                    (_Float16)1.0f);
+        const _Float16 l1 = __builtin_amdgcn_fmed3h((_Float16)__builtin_fmaf((float)h[1], m1, v1), (_Float16)0.0f,
+                                                    (_Float16)1.0f);
+        lw[q] = __builtin_bit_cast(uint32_t, (f16x2v){l0, l1});
+        hw[q] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2v, h), (s16x2v){0, 0}));
+    }
+    hi = __builtin_bit_cast(f16x8, hw);
+    lo = __builtin_bit_cast(f16x8, lw);
+}
+
+struct X3W {
+    f16x8 h0, h1, l0, l1;  // hi / residual A operands of k-steps 0, 1
+    f32x16 b;
+};
+__device__ __forceinline__ X3W x3_load(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int jl) {
+    const int lane = lane_id(), h = lane >> 5;
+    const f16x8 *A = reinterpret_cast<const f16x8 *>(lp + X3_HID + jl * X3_HSTRIDE);
+    return X3W{A[lane], A[64 + lane], A[128 + lane], A[192 + lane], load_bias16(fl + 32 + 32 * jl + 16 * h)};
+}
+
+template <int NT>
+__device__ __forceinline__ void hidden_x3(const X3W &w, f32x16 (&acc)[NT], float m1) {
+    f16x8 hi[NT][2], lo[NT][2];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) split_x3(acc[t], s, m1, hi[t][s], lo[t][s]);
+    // small terms first (the bias, then the residual products), the hi.hi product last
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h0, lo[t][0], w.b, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h1, lo[t][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.l0, hi[t][0], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.l1, hi[t][1], d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h0, hi[t][0], d, 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.h1, hi[t][1], d, 0, 0, 0);
+    }
+}
+
+template <int NT, int NH>
+__device__ __forceinline__ float mlp32_x3_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                             int nh_rt, float fr, float x, float y, float z) {
+    constexpr int P = NR_PRECISION_FP16;
+    const int nh = NH > 0 ? NH : nh_rt;
+    const int lane = lane_id(), h = lane >> 5;
+    const float *F = fl + x3_final(nh);
+    const float m1 = F[33];
+    f32x16 acc[NT];
+    {
+        // layer 0 as the reduced-precision MLP's (mlp32_lowp_nt) on the inputs scaled by
+        // 2^X3_XYZ_SHIFT (exact): hi/lo fp16 split, one K = 16 MFMA per tile
+        const float sx = F[34];
+        x *= sx; y *= sx; z *= sx;
+        const uint32_t p0 = cvt2<P>(x, y);
+        const float dx = x - lo16f<P>(p0), dy = y - hi16f<P>(p0);
+        const uint32_t q = cvt2<P>(z, dx);
+        const uint32_t r = cvt2<P>(dy, z - lo16f<P>(q));
+        uint32_t f = 0;
+        if (in0 == 4) {
+            const uint32_t f0 = cvt2<P>(fr, 0.0f);
+            f = cvt2<P>(fr, fr - lo16f<P>(f0));
+        }
+        const uint32_t qf = (q & 0xffffu) | (f << 16);
+        const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
+        const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
+        const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
+        const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
+        const f16x8 A = reinterpret_cast<const f16x8 *>(lp)[lane];
+        const f32x16 b0 = load_bias16(fl + 16 * h);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, __builtin_bit_cast(f16x8, (u32x4){w0[t], w1[t], w2[t], w3[t]}),
+                                                            b0, 0, 0, 0);
+    }
+    if constexpr (NH > 0) {
+#pragma unroll
+        for (int jl = 0; jl < NH; ++jl) hidden_x3<NT>(x3_load(lp, fl, jl), acc, m1);
+    } else {
+        for (int jl = 0; jl < nh; ++jl) hidden_x3<NT>(x3_load(lp, fl, jl), acc, m1);
+    }
+    // final 32 -> 1 layer in f32 on the VALU: lane l holds 16 of point (l & 31)'s units, the
+    // pack holds their (scaled-back) weights in register order; the halves' partial sums are
+    // joined by one v_permlane32_swap (tile 1 to lanes 32-63 on the way)
+    const float4 *W4 = reinterpret_cast<const float4 *>(F + 16 * h);
+    const float4 wa = W4[0], wb = W4[1], wc = W4[2], wd = W4[3];
+    const float wf[16] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w, wc.x, wc.y, wc.z, wc.w, wd.x, wd.y, wd.z, wd.w};
+    float zt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        float a = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a = __builtin_fmaf(wf[i], fmaxf(acc[t][i], 0.0f), a);
+        zt[t] = a;
+    }
+    float z0, z1;
+    if constexpr (NT == 1) {
+        half_views(zt[0], z0, z1);
+    } else {
+        const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
+        z0 = __uint_as_float(rr[0]);
+        z1 = __uint_as_float(rr[1]);
+    }
+    return (z0 + z1) + F[32];
+}
+
+// wave-uniform: every lane's inputs are within the fp32x3 pack's bounds (NaN is not)
+__device__ __forceinline__ bool inputs_in_bound_x3(float x, float y, float z, float f) {
+    const bool ok = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
+                    __builtin_fabsf(z) <= X3_INPUT_BOUND && __builtin_fabsf(f) <= X3_FRAME_BOUND;
+    return __ballot(!ok) == 0;
+}
+
+// ok (wave-uniform): the fp32x3 pack exists (M.lp_clamp) and every input of the call is within
+// its bounds; otherwise the fp32 MLP (bit-exact, from the fp32 pack) evaluates the wave
+__device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, const uint16_t *lp, const float *fl,
+                                          float fr, float x, float y, float z, uint32_t tmask, bool ok) {
+    if (!ok) return mlp16_fp32(M, s32, fr, x, y, z, tmask);
+    if (M.nh == 7) {
+        if (tmask & 0xcu) return mlp32_x3_nt<2, 7>(lp, fl, M.in0, M.nh, fr, x, y, z);
+        return mlp32_x3_nt<1, 7>(lp, fl, M.in0, M.nh, fr, x, y, z);
+    }
+    if (tmask & 0xcu) return mlp32_x3_nt<2, 0>(lp, fl, M.in0, M.nh, fr, x, y, z);
+    return mlp32_x3_nt<1, 0>(lp, fl, M.in0, M.nh, fr, x, y, z);
+}
+
+// cl: see mlp16_lowp (ignored in fp32); fp32x3: the pack is valid (M.lp_clamp), the inputs are
+// checked here
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
     if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
+    if (prec == NR_PRECISION_FP32X3)
+        return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0 && inputs_in_bound_x3(x, y, z, fr));
     return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }
 

@@ -247,6 +247,118 @@ bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<fl
     return true;
 }
 
+// fp32x3 (nr_internal.h X3_*, nr_mlp16.h mlp32_x3_nt).  Interval bounds in double over the
+// exact f32 weights for xyz within +-X3_INPUT_BOUND (and a 4th input within +-X3_FRAME_BOUND)
+// give each ReLU layer's top activation; layer l's activations are scaled by 2^-e[l] with
+// e[l] = ceil(log2(top)) - 10, so a scaled activation stays below 2^10 (x2 margin for the
+// evaluation's rounding against the 2^11 the residual clamp needs).  Weights of layer l are
+// scaled by 2^(e[l-1] - e[l]) and split into fp16 hi + residual; layer 0's xyz weights by
+// 2^(-e[0] - X3_XYZ_SHIFT) (the kernel scales the inputs by 2^X3_XYZ_SHIFT), its 4th-input
+// weights by 2^-e[0]; the final layer keeps f32 weights times 2^e[last].  Every scaling is by a
+// power of two, so the split approximates the unscaled network; the fp16 range limits it
+// (hi below 2^15), otherwise ok = 0 and the kernels run the fp32 MLP.
+bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                const std::vector<std::vector<float>> &B, std::vector<uint16_t> &a_ops, std::vector<float> &fl,
+                int *ok_out) {
+    if (!fused_shape_ok(dims)) return false;
+    const int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
+    a_ops.assign((size_t)x3_elems(nh), 0);
+    fl.assign((size_t)x3_floats(nh), 0.0f);
+    bool ok = true;
+    std::vector<int> e(nl - 1, 0);
+    {
+        std::vector<double> lo(in0), hi(in0);
+        for (int i = 0; i < in0; ++i) {
+            const double b = i < 3 ? (double)X3_INPUT_BOUND : (double)X3_FRAME_BOUND;
+            lo[i] = -b;
+            hi[i] = b;
+        }
+        for (int l = 0; l < nl - 1 && ok; ++l) {
+            const int in = dims[l], out = dims[l + 1];
+            std::vector<double> nlo(out), nhi(out);
+            double top = 0.0;
+            for (int u = 0; u < out; ++u) {
+                double a = B[l][u], b = B[l][u];
+                for (int i = 0; i < in; ++i) {
+                    const double w = K[l][(size_t)i * out + u];
+                    a += std::min(w * lo[i], w * hi[i]);
+                    b += std::max(w * lo[i], w * hi[i]);
+                }
+                nlo[u] = std::max(a, 0.0);
+                nhi[u] = std::max(b, 0.0);
+                top = std::max(top, nhi[u]);
+            }
+            if (!std::isfinite(top)) ok = false;
+            e[l] = top > 0.0 ? (int)std::ceil(std::log2(top)) - 10 : 0;
+            if (e[l] < -100 || e[l] > 100) ok = false;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    const int ex = X3_XYZ_SHIFT;
+    // fp16 hi / residual of a scaled weight; every hi must stay below 2^15
+    auto split = [&](double ws, uint16_t &h, uint16_t &l) {
+        if (!(std::fabs(ws) < 32768.0)) ok = false;
+        const float w = (float)ws;  // exact: a power-of-two multiple of an f32 weight (range checked)
+        h = f2fp16(w);
+        l = f2fp16(w - fp16f(h));
+    };
+    auto crow = [](int h, int i) { return (i & 3) + 8 * (i >> 2) + 4 * h; };  // C/D row of register i
+    auto kin = [](int s, int h, int k) { return 16 * s + 8 * (k >> 2) + 4 * h + (k & 3); };
+    // layer 0, K = 16, as pack_lowp_32: h = 0 {wh x3 . xh, wh x3 . xl, wh3 . fh, wh3 . fl},
+    //                                  h = 1 {wl x3 . xh, wl3 . fh, 0 x4}
+    for (int lane = 0; lane < 64; ++lane) {
+        const int m = lane & 31, h = lane >> 5;
+        uint16_t *el = &a_ops[(size_t)lane * 8];
+        for (int c = 0; c < in0; ++c) {
+            const double ws = std::ldexp((double)K[0][(size_t)c * 32 + m], -e[0] - (c < 3 ? ex : 0));
+            uint16_t wh, wl;
+            split(ws, wh, wl);
+            if (c < 3) {
+                if (h == 0) el[c] = el[3 + c] = wh;
+                else el[c] = wl;
+            } else {
+                if (h == 0) el[6] = el[7] = wh;
+                else el[3] = wl;
+            }
+        }
+    }
+    for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 16; ++i) fl[h * 16 + i] = (float)std::ldexp((double)B[0][crow(h, i)], -e[0]);
+    for (int j = 0; j < nh; ++j) {
+        const std::vector<float> &Kj = K[j + 1];
+        const int sw = e[j] - e[j + 1];
+        for (int s = 0; s < 2; ++s)
+            for (int lane = 0; lane < 64; ++lane)
+                for (int k = 0; k < 8; ++k) {
+                    const int m = lane & 31, h = lane >> 5;
+                    const size_t o = (size_t)X3_HID + (size_t)j * X3_HSTRIDE + (size_t)s * 512 + lane * 8 + k;
+                    split(std::ldexp((double)Kj[(size_t)kin(s, h, k) * 32 + m], sw), a_ops[o], a_ops[o + 1024]);
+                }
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) fl[32 + 32 * j + h * 16 + i] = (float)std::ldexp((double)B[j + 1][crow(h, i)], -e[j + 1]);
+    }
+    const int fo = x3_final(nh);
+    for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < 16; ++i) {
+            const double w = std::ldexp((double)K[nl - 1][crow(h, i)], e[nl - 2]);
+            if (K[nl - 1][crow(h, i)] != 0.0f && !(std::fabs(w) > 0x1p-120 && std::fabs(w) < 0x1p120)) ok = false;
+            fl[fo + h * 16 + i] = (float)w;
+        }
+    fl[fo + 32] = B[nl - 1][0];
+    fl[fo + 33] = -1.0f;
+    fl[fo + 34] = std::ldexp(1.0f, ex);
+    fl[fo + 35] = 1.0f;
+    // scaled biases must stay normal f32 (power-of-two scaling exact)
+    for (int l = 0; l < nl - 1; ++l)
+        for (float b : B[l]) {
+            const double bs = std::ldexp((double)b, -e[l]);
+            if (b != 0.0f && !(std::fabs(bs) > 0x1p-120 && std::fabs(bs) < 0x1p120)) ok = false;
+        }
+    if (ok_out) *ok_out = ok ? 1 : 0;
+    return true;
+}
+
 // updateViewMatrices (reference src/main.cpp:207-222), evaluated in double and
 // rounded to float once (the reference uses Eigen float arithmetic).
 void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {

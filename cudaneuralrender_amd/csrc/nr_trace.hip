@@ -143,8 +143,14 @@ __device__ __forceinline__ void set_priority(int prio) {
 // frame's pixels fill the freed slots; every ray carries its frame index (rf) and the
 // frame-dependent values (camera, sphere offset, animation input, output image) come
 // from the FrameArgs staged in LDS.
+// fp32x3: its MLP holds the hi and residual operands of two tiles besides the accumulators;
+// 3 workgroups per CU (<= 168 VGPRs) keep it out of scratch
+#ifndef NR_TRACE_BPC_X3
+#define NR_TRACE_BPC_X3 3
+#endif
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
-__global__ __launch_bounds__(256, (PREC != NR_PRECISION_FP32 || BATCH) ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
+                                  : (PREC != NR_PRECISION_FP32 || BATCH) ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
@@ -484,12 +490,15 @@ __global__ __launch_bounds__(256, (PREC != NR_PRECISION_FP32 || BATCH) ? NR_TRAC
 #ifndef NR_MLP16_WPS
 #define NR_MLP16_WPS 5
 #endif
+#ifndef NR_MLP16_WPS_X3
+#define NR_MLP16_WPS_X3 4
+#endif
 // Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
 // matrix-core tiles: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks; the next
 // chunk's inputs are loaded before the current chunk's MLP, so their HBM latency (~2 us)
 // hides behind its MFMAs instead of stalling every wave once per chunk.
 template <int PREC>
-__global__ __launch_bounds__(256, NR_MLP16_WPS) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
+__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3 : NR_MLP16_WPS) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     // the wave's chunk index is uniform: readfirstlane keeps the loop control (base, rem,
@@ -565,6 +574,8 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         hipLaunchKernelGGL(k_mlp16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
     else if (prec == NR_PRECISION_FP16)
         hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
+    else if (prec == NR_PRECISION_FP32X3)
+        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP32X3>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
     else
         hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP32>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
     return hipGetLastError();
@@ -577,6 +588,8 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else if (prec == NR_PRECISION_FP16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP32X3)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, true>), dim3(grid), dim3(256), sm, st, A, M, T);
     } else if (T.nframes > 0) {
@@ -584,6 +597,8 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else if (prec == NR_PRECISION_FP16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP32X3)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
     } else if (T.stamps) {
@@ -591,6 +606,8 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else if (prec == NR_PRECISION_FP16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP32X3)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
     } else {
@@ -598,6 +615,8 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
         else if (prec == NR_PRECISION_FP16)
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_FP32X3)
+            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false>), dim3(grid), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false>), dim3(grid), dim3(256), sm, st, A, M, T);
     }

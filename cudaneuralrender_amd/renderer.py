@@ -243,6 +243,7 @@ class Renderer:
 
     def set_debug(self, flags):
         self._chk(self._L.nr_set_debug(self._ctx, int(flags)))
+        return self
 
     def debug_stamps(self):
         """Per-wave stamps of the last k_trace: {start, queue drained, end (100 MHz ticks),

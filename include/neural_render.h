@@ -38,6 +38,10 @@ extern "C" {
 #define NR_PRECISION_FP32 0  /* bit-exact with the CPU oracle (f32 MFMA = fmaf chain) */
 #define NR_PRECISION_BF16 1  /* bf16 MFMA, f32 accumulate; normals evaluated in fp32 */
 #define NR_PRECISION_FP16 2  /* fp16 MFMA, f32 accumulate; normals evaluated in fp32 */
+#define NR_PRECISION_FP32X3 3 /* fp32-class on the fp16 matrix core: three-term split a.w ~ ah.wh + al.wh + ah.wl,
+                                  f32 accumulate (~2-3x the f32 chain's error against an exact
+                                  evaluation); normals evaluated in fp32 (bit-exact); waves with
+                                  inputs outside the pack's bounds run the fp32 MLP */
 
 /* scene composition, sceneSDF (volumeRender_kernel.cu:217-230) */
 #define NR_SCENE_V1 0        /* v1: manySphere(p, nSDF, true) -- 9-sphere smooth union (:222) */
@@ -199,7 +203,7 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = the plain ReLU
  * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
  * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and
- * A/B of the two forms).  Bit 10 = nr_render_batch deals its pixel queue frame after
+ * A/B of the two forms); fp32x3 by the fp32 MLP for every wave (its fallback, bit-exact fp32).  Bit 10 = nr_render_batch deals its pixel queue frame after
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)

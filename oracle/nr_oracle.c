@@ -65,6 +65,7 @@
 #endif
 
 #define OR_MAX_LAYERS 32
+#define OR_MAX_WIDTH 4096   /* widest layer precision 3 takes */
 
 typedef struct { float x, y, z; } f3;
 
@@ -219,9 +220,36 @@ static void mlp_point_gpu_lowp(const or_mlp *m, const or_lowp *q, const float *x
     y[0] = (half[0] + half[1]) + m->b[nl - 1][0];
 }
 
+/* precision 3: the network evaluated exactly (fp64 products and sums, ReLU in fp64), the output
+ * rounded once to f32 -- the arithmetic-independent value every fp32-class evaluation order
+ * (CUTLASS's unpinned SIMT order, the fp32x3 matrix-core split, ...) approximates.  Used to
+ * measure how far any fp32-class MLP may legitimately move a frame from the fp32 contract
+ * (tests/test_gpu_fp32x3.py). */
+static void mlp_point_f64(const or_mlp *m, const float *x, float *y)
+{
+    double a[OR_MAX_WIDTH], z[OR_MAX_WIDTH];
+    for (int k = 0; k < m->dims[0]; ++k) a[k] = x[k];
+    for (int l = 0; l < m->nlayers; ++l) {
+        int in = m->dims[l], out = m->dims[l + 1], last = (l == m->nlayers - 1);
+        for (int o = 0; o < out; ++o) {
+            const float *w = m->W[l] + (size_t)o * in;
+            double acc = 0.0;
+            for (int k = 0; k < in; ++k) acc += (double)w[k] * a[k];
+            acc += m->b[l][o];
+            z[o] = last ? acc : (acc > 0.0 ? acc : 0.0);
+        }
+        for (int o = 0; o < out; ++o) a[o] = z[o];
+    }
+    for (int o = 0; o < m->dims[m->nlayers]; ++o) y[o] = (float)a[o];
+}
+
 static void mlp_point(const or_mlp *m, const or_lowp *q, const float *x, float *y, float *buf0, float *buf1,
                       int precision)
 {
+    if (precision == 3) {
+        mlp_point_f64(m, x, y);
+        return;
+    }
     if (precision != 0 && q) {
         mlp_point_gpu_lowp(m, q, x, y);
         return;
@@ -287,7 +315,8 @@ int or_mlp_forward(int nlayers, const int *dims, const float *params,
     if (in_stride < dims[0]) return -2;
     int out = dims[nlayers];
     or_lowp q, *qp = NULL;
-    if (precision != 0 && fused_shape(&m)) {
+    if (precision == 3 && m.maxw > OR_MAX_WIDTH) return -3;
+    if ((precision == 1 || precision == 2) && fused_shape(&m)) {
         if (lowp_init(&q, &m, precision)) return -3;
         qp = &q;
     }
@@ -592,7 +621,8 @@ static int intersectSphere(f3 o, f3 d, float r, float *tnear, float *tfar) /* :1
  * evaluations (4 per coloured ray), stats[2] = host iterations executed,
  * stats[3] = rays that hit the bounding sphere, stats[4] = coloured pixels. */
 /* or_render_ex: `precision` 1/2 marches with the GPU's bf16/fp16 MLP arithmetic
- * (mlp_point_gpu_lowp; normals stay fp32, as on the GPU), and only rows [y0, y1) of the
+ * (mlp_point_gpu_lowp; normals stay fp32, as on the GPU), 3 with the exact (fp64) MLP
+ * (mlp_point_f64; normals fp32), and only rows [y0, y1) of the
  * W x H frame are rendered into out ((y1 - y0) x W) -- a crop of the full frame with the
  * full frame's rays. */
 int or_render_ex(int nlayers, const int *dims, const float *params,
@@ -626,13 +656,14 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
     if (dims[0] != num_inputs || dims[nlayers] != 1) return -3;
     if (color_type == 1 && (!matcap || mw < 1 || mh < 1)) return -4;
     if (y0 < 0 || y1 > H || y0 > y1) return -6;
-    if (precision != 0 && !fused_shape(&m)) return -7;
+    if ((precision == 1 || precision == 2) && !fused_shape(&m)) return -7;
+    if (precision == 3 && m.maxw > OR_MAX_WIDTH) return -7;
     or_settings S = { inv_view, normal, frame, color_type, num_inputs, scene, matcap, mw, mh };
     long npix = (long)W * (y1 - y0);
     long long st[5] = { 0, 0, 0, 0, 0 };
     if (npix <= 0) { if (stats) memcpy(stats, st, sizeof st); return 0; }
     or_lowp q, *qp = NULL;
-    if (precision != 0) {
+    if (precision == 1 || precision == 2) {
         if (lowp_init(&q, &m, precision)) return -5;
         qp = &q;
     }

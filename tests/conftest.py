@@ -31,3 +31,22 @@ def nets():
     """(dims, kernels, biases) for every bundled geometry, read by libnr's HDF5 reader."""
     import cudaneuralrender_amd as nr
     return {g: nr.read_keras_h5(nr.geometry_path(g)) for g in GEOMS}
+
+
+def channels(img):
+    """uint32 RGBA (a<<24|b<<16|g<<8|r) -> [..., 4] int channels"""
+    import numpy as np
+    return np.stack([(img >> (8 * c)) & 0xff for c in range(4)], -1).astype(np.int32)
+
+
+def compare_frames(gpu, ref):
+    """Identical-pixel fraction, coverage IoU and per-channel mean / max |delta| over the pixels
+    both frames cover."""
+    import numpy as np
+    fg, fr = gpu != 0, ref != 0
+    both = fg & fr
+    d = np.abs(channels(gpu) - channels(ref))[both] if both.any() else np.zeros((0, 4), np.int32)
+    return {"identical": float((gpu == ref).mean()),
+            "iou": float(both.sum() / max((fg | fr).sum(), 1)),
+            "mean_abs": [round(float(v), 4) for v in (d.mean(0) if len(d) else np.zeros(4))],
+            "max_abs": [int(v) for v in (d.max(0) if len(d) else np.zeros(4))]}

@@ -49,3 +49,23 @@ def test_random_poses():
     p = bench.random_poses()
     assert len(p) == 8 and p == bench.random_poses()
     assert all(-30 <= rx <= 30 and 0 <= ry < 360 for rx, ry in p)
+
+
+def test_config_presets(monkeypatch):
+    """--config picks a BASELINE config; explicit flags override it; c5 is replicas."""
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert (a.config, a.geometry, a.size, a.precision, a.max_steps, a.replicas) == ("c2", "plane_1", 1024, "fp32", 128, False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "c3", "--size", "512"])
+    a = bench.parse()
+    assert (a.geometry, a.size, a.precision, a.max_steps) == ("car_1", 512, "bf16", 256)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "c5", "--gpus", "8"])
+    a = bench.parse()
+    assert a.replicas and a.geometry is None and (a.size, a.precision) == (2048, "fp16")
+
+
+def test_c5_rank_geometries():
+    """c5: rank r renders bundled geometry r % 5 (BASELINE configs[4], one geometry per GPU)."""
+    g = [bench.GEOMS[r % len(bench.GEOMS)] for r in range(8)]
+    assert g[:5] == bench.GEOMS and g[5:] == bench.GEOMS[:3]
+    assert all(os.path.exists(os.path.join(REPO, "data", "neuralGeometries", x + ".h5")) for x in bench.GEOMS)

@@ -16,7 +16,9 @@ import torch  # noqa: E402
 
 import cudaneuralrender_amd as nr  # noqa: E402
 
-PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}
+PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6, "fp32x3": 2516.6}
+# matrix-core FLOP issued per algorithmic FLOP of the hidden layers (fp32x3: three fp16 terms)
+ISSUED = {"fp32": 1, "bf16": 1, "fp16": 1, "fp32x3": 3}
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1 << 22)
 ap.add_argument("--iters", type=int, default=20)
@@ -45,7 +47,7 @@ for prec in (["fp32", "bf16", "fp16"] if a.precision == "all" else a.precision.s
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
         tf = a.n * 14592 / (ms * 1e-3) / 1e12
-        util = a.n * 14336 / (ms * 1e-3) / 1e12 / PEAK[prec]
-        res.append({"precision": prec, "debug": a.debug, "tile": "16" if prec == "fp32" else "32", "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
+        util = a.n * 14336 * ISSUED[prec] / (ms * 1e-3) / 1e12 / PEAK[prec]
+        res.append({"precision": prec, "debug": a.debug, "tile": "16" if prec == "fp32" else "32", "issued_per_flop": ISSUED[prec], "blocks_per_cu": bpc, "n": a.n, "ms": round(ms, 4), "TFLOPs": round(tf, 2),
                     "hidden_layer_mfma_util": round(util, 4), "Gpoints_per_s": round(a.n / ms / 1e6, 2)})
         print(json.dumps(res[-1]), flush=True)
