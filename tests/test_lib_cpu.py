@@ -186,3 +186,134 @@ def test_batch_frames_per_launch_fits_the_queue_counters():
             assert (k + 1) * per_frame + 256 * 8 * 4 * 64 >= 2 ** 32
     assert f(16384, 16384, 1, 1, 0, 16, 1) == 15
     assert f(0, 16, 1, 1, 0, 4) == 0
+
+
+_REG = re.compile(r"\b([va])(?:\[(\d+):(\d+)\]|(\d+)(?!\w))")
+
+
+def _regs(ops):
+    """{('v'|'a', index)} named by an operand string (v7, v[8:11], a[0:15])"""
+    out = set()
+    for kind, lo, hi, one in _REG.findall(ops):
+        lo, hi = (int(lo), int(hi)) if lo else (int(one), int(one))
+        out |= {(kind, i) for i in range(lo, hi + 1)}
+    return out
+
+
+def _parse(line):
+    """(address, mnemonic, dst regs, src regs) of one llvm-objdump -d line, or None"""
+    m = re.match(r"\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-F]+):", line)
+    if not m:
+        return None
+    mn, ops, addr = m.group(1), m.group(2), int(m.group(3), 16)
+    parts = [p.strip() for p in re.split(r",(?![^\[]*\])", ops)] if ops else []
+    dst = _regs(parts[0]) if parts and not mn.startswith(("s_", "ds_write", "global_store", "buffer_store")) else set()
+    src = set().union(*[_regs(p) for p in parts[1:]]) if len(parts) > 1 else set()
+    return addr, mn, dst, src
+
+
+def _wait_states(mn, line):
+    m = re.match(r"\s+s_nop\s+(?:0x)?([0-9a-f]+)", line)
+    return int(m.group(1), 16) + 1 if m else 1
+
+
+def check_clamp_runs(lines):
+    """Checks every v_cvt_pk_bf16_f32 ... clamp run of one disassembly (test below); returns the count."""
+    runs_checked = 0
+    ins = [(ln, _parse(ln)) for ln in lines]
+    ins = [(ln, x) for ln, x in ins if x]
+    # predecessors of every instruction: the one before it (unless that one is an
+    # unconditional jump or the end of the program) and every branch that targets it
+    addr_ix = {x[0]: n for n, (_, x) in enumerate(ins)}
+    preds = {n: ([n - 1] if n > 0 and ins[n - 1][1][1] not in ("s_branch", "s_endpgm") else [])
+             for n in range(len(ins))}
+    for n, (ln, (addr, mn, _, _)) in enumerate(ins):
+        m = re.match(r"\s+s_(?:c)?branch\w*\s+(-?\d+)", ln)
+        if m:
+            off = int(m.group(1))
+            off = off - 65536 if off >= 32768 else off
+            t = addr_ix.get(addr + 4 + 4 * off)
+            if t is not None:
+                preds[t].append(n)
+    i = 0
+    while i < len(ins):
+        if not (ins[i][1][1] == "v_cvt_pk_bf16_f32" and " clamp" in ins[i][0]):
+            i += 1
+            continue
+        j = i
+        while j < len(ins) and ins[j][1][1] == "v_cvt_pk_bf16_f32" and " clamp" in ins[j][0]:
+            j += 1
+        run = ins[i:j]
+        S = set().union(*[x[3] for _, x in run])
+        D = set().union(*[x[2] for _, x in run])
+        where = f"run @ {run[0][1][0]:#x}"
+        # backward walk over every path into the run, up to 24 wait states deep
+        stack, seen = [(k, 0, frozenset()) for k in preds[i]], set()
+        while stack:
+            k, W, read_since = stack.pop()
+            if (k, W, read_since) in seen:
+                continue
+            seen.add((k, W, read_since))
+            ln, (addr, mn, dst, src) = ins[k]
+            if mn.startswith("v_mfma") and (dst & (S | D) or src & D):
+                assert dst & read_since, f"{where}: MFMA at {addr:#x} ({W} wait states before) not touched"
+                continue  # the touched MFMA completed, and every MFMA of this path before it
+            if mn.startswith("v_") and not mn.startswith("v_mfma"):
+                read_since = read_since | frozenset(src)
+            W += _wait_states(mn, ln)
+            if W < 24:
+                stack.extend((q, W, read_since) for q in preds[k])
+        # forward: first MFMA reading a result of the run
+        W, k = 0, j
+        while k < len(ins):
+            ln, (addr, mn, dst, src) = ins[k]
+            if mn.startswith("v_mfma") and src & D:
+                assert W >= 2, f"{where}: MFMA {W} wait states after the run"
+                break
+            if mn.startswith(("s_branch", "s_cbranch", "s_endpgm")):
+                break
+            W += _wait_states(mn, ln)
+            k += 1
+        runs_checked += 1
+        i = j
+    return runs_checked
+
+
+def test_bf16_clamp_conversions_are_hazard_free(tmp_path):
+    """the bf16 ReLU folded into the conversion is inline asm (nr_mlp16.h
+    relu_clamp_bf16_x*), invisible to the compiler's hazard recognizer.  Its safety rests on a
+    VALU 'touch' of every accumulator the block converts (the compiler puts the MFMA -> VALU wait
+    states before the touch) and on the block's trailing s_nop 1 (a VALU write needs 2 wait
+    states before an MFMA reads it).  Checked on the generated code of every instance:
+      * on every path into each run of v_cvt_pk_bf16_f32 ... clamp (control flow followed
+        through branches and branch targets), the most recent MFMA that writes a register the run
+        reads, or reads or writes a register the run writes, is followed before the run by a VALU
+        read of its result (the touch); a path is followed until 24 wait states separate it from
+        the run (beyond every MFMA hazard window);
+      * the first MFMA after the run that reads one of its results is >= 2 wait states after it."""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    so = tmp_path / "libnr.so"
+    shutil.copy(_lib.LIB_PATH, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    objs = sorted(p for p in tmp_path.iterdir() if "amdgcn" in p.name and "gfx950" in p.name)
+    assert objs
+    runs, caught = 0, 0
+    for p in objs:
+        lines = subprocess.run([objdump, "-d", str(p)], check=True, capture_output=True, text=True).stdout.splitlines()
+        n = check_clamp_runs(lines)
+        runs += n
+        if n:
+            # the checker itself: without the touches (v_and_b32 vX, 1, vY) it must object
+            # wherever a run reads MFMA results in place (runs that read v_accvgpr_read copies
+            # of AGPR accumulators are safe without them: the copies are the touch)
+            cut = [ln for ln in lines if not re.match(r"\s+v_and_b32_e32 v\d+, 1, v\d+\s", ln)]
+            try:
+                check_clamp_runs(cut)
+            except AssertionError as e:
+                assert "not touched" in str(e)
+                caught += 1
+    assert runs > 0 and caught > 0
