@@ -268,13 +268,13 @@ bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<floa
     std::vector<int> e(nl - 1, 0);
     {
         // The bound is the maximum of the interval bounds over a grid of sub-boxes of the input
-        // box (16 per xyz axis; 12 per axis x 4 frame slabs for a 4th input): still a hard bound,
+        // box (16 per xyz axis; 8 per axis x 16 frame slabs for a 4th input): still a hard bound,
         // 2-4 binades tighter than one interval pass over the whole box on the bundled networks.
         // Activations then sit higher in the window below 2^10, so fewer residuals al = a - ah
         // fall into fp16's subnormal range, which would cost them relative precision (emulated:
         // mean error vs fp64 from 2.4-3.9x to 1.8-2.4x the f32 chain's, a random 4-input
         // network 5.8x -> 3.1x; tests/test_gpu_fp32x3.py).
-        const int mx = in0 == 4 ? 12 : 16, mf = in0 == 4 ? 4 : 1;
+        const int mx = in0 == 4 ? 8 : 16, mf = in0 == 4 ? 16 : 1;
         std::vector<double> top(nl - 1, 0.0), lo, hi, nlo, nhi;
         for (int box = 0; box < mx * mx * mx * mf && ok; ++box) {
             lo.assign(in0, 0.0);

@@ -97,3 +97,27 @@ def test_animation_clamp_frame_bound(rend, chrome):
             assert sa["ray_steps"] == sb["ray_steps"]
     finally:
         rend.set_precision("fp32").set_static(nr.NR_COLOR_MATCAP, 3).set_view(iv, nm, 0)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("debug", [0, NO_CLAMP])
+def test_mlp_128_point_form_equals_64_point_form(rend, nets, prec, debug):
+    """k_mlp16 runs bf16/fp16 on 128 points per wave (nr_mlp16.h mlp32_lowp_128: four 32-point
+    tiles from two points per lane); a call of at most 64 points takes the 64-point form
+    (mlp32_lowp_nt, the tracers' MLP).  Same arithmetic per point: every point's value is the
+    same bit for bit, whichever tile, lane half and chunk carries it (ragged ends included)."""
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec).set_debug(debug)
+    try:
+        X = np.random.default_rng(11).uniform(-1.3, 1.3, size=(64 * 24 + 37, 3)).astype(np.float32)
+        X[5 * 64 + 9] = (2e6, 0.0, 0.0)  # beyond LP_INPUT_BOUND: this 128-point chunk takes the max form
+        big = rend.mlp_forward(X)
+        for c0 in range(0, len(X), 64):
+            small = rend.mlp_forward(X[c0:c0 + 64])
+            assert np.array_equal(big[c0:c0 + 64], small), (c0, np.abs(big[c0:c0 + 64] - small).max())
+        # and 65..127-point calls: a 128-point chunk whose second set is ragged
+        for n in (65, 100, 127):
+            assert np.array_equal(rend.mlp_forward(X[:n]), big[:n]), n
+    finally:
+        rend.set_debug(0)
+        rend.set_precision("fp32")
