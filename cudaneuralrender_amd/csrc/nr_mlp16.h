@@ -312,6 +312,39 @@ __device__ __forceinline__ void relu_clamp_bf16_x2(const f32x16 &c, const f32x16
           "v"(d[8]), "v"(d[9]), "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15]),
           "v"(t0), "v"(t1));
 }
+// four tiles (the 128-point MLP): one block, so that no MFMA of the next layer can be scheduled
+// between the conversions of two tile pairs while the pair not yet converted is read
+__device__ __forceinline__ void relu_clamp_bf16_x4(const f32x16 &c0, const f32x16 &c1, const f32x16 &c2, const f32x16 &c3,
+                                                   u32x4 (&k)[4][2]) {
+    const uint32_t t0 = __float_as_uint(c0[0]) & 1u, t1 = __float_as_uint(c1[0]) & 1u;  // the touches
+    const uint32_t t2 = __float_as_uint(c2[0]) & 1u, t3 = __float_as_uint(c3[0]) & 1u;
+    asm(NR_CVC(0, 32, 33) NR_CVC(1, 34, 35) NR_CVC(2, 36, 37) NR_CVC(3, 38, 39)
+         NR_CVC(4, 40, 41) NR_CVC(5, 42, 43) NR_CVC(6, 44, 45) NR_CVC(7, 46, 47)
+         NR_CVC(8, 48, 49) NR_CVC(9, 50, 51) NR_CVC(10, 52, 53) NR_CVC(11, 54, 55)
+         NR_CVC(12, 56, 57) NR_CVC(13, 58, 59) NR_CVC(14, 60, 61) NR_CVC(15, 62, 63)
+         NR_CVC(16, 64, 65) NR_CVC(17, 66, 67) NR_CVC(18, 68, 69) NR_CVC(19, 70, 71)
+         NR_CVC(20, 72, 73) NR_CVC(21, 74, 75) NR_CVC(22, 76, 77) NR_CVC(23, 78, 79)
+         NR_CVC(24, 80, 81) NR_CVC(25, 82, 83) NR_CVC(26, 84, 85) NR_CVC(27, 86, 87)
+         NR_CVC(28, 88, 89) NR_CVC(29, 90, 91) NR_CVC(30, 92, 93) NR_CVC(31, 94, 95)
+        "s_nop 1"
+        : "=&v"(k[0][0][0]), "=&v"(k[0][0][1]), "=&v"(k[0][0][2]), "=&v"(k[0][0][3]),
+          "=&v"(k[0][1][0]), "=&v"(k[0][1][1]), "=&v"(k[0][1][2]), "=&v"(k[0][1][3]),
+          "=&v"(k[1][0][0]), "=&v"(k[1][0][1]), "=&v"(k[1][0][2]), "=&v"(k[1][0][3]),
+          "=&v"(k[1][1][0]), "=&v"(k[1][1][1]), "=&v"(k[1][1][2]), "=&v"(k[1][1][3]),
+          "=&v"(k[2][0][0]), "=&v"(k[2][0][1]), "=&v"(k[2][0][2]), "=&v"(k[2][0][3]),
+          "=&v"(k[2][1][0]), "=&v"(k[2][1][1]), "=&v"(k[2][1][2]), "=&v"(k[2][1][3]),
+          "=&v"(k[3][0][0]), "=&v"(k[3][0][1]), "=&v"(k[3][0][2]), "=&v"(k[3][0][3]),
+          "=&v"(k[3][1][0]), "=&v"(k[3][1][1]), "=&v"(k[3][1][2]), "=&v"(k[3][1][3])
+        : "v"(c0[0]), "v"(c0[1]), "v"(c0[2]), "v"(c0[3]), "v"(c0[4]), "v"(c0[5]), "v"(c0[6]), "v"(c0[7]),
+          "v"(c0[8]), "v"(c0[9]), "v"(c0[10]), "v"(c0[11]), "v"(c0[12]), "v"(c0[13]), "v"(c0[14]), "v"(c0[15]),
+          "v"(c1[0]), "v"(c1[1]), "v"(c1[2]), "v"(c1[3]), "v"(c1[4]), "v"(c1[5]), "v"(c1[6]), "v"(c1[7]),
+          "v"(c1[8]), "v"(c1[9]), "v"(c1[10]), "v"(c1[11]), "v"(c1[12]), "v"(c1[13]), "v"(c1[14]), "v"(c1[15]),
+          "v"(c2[0]), "v"(c2[1]), "v"(c2[2]), "v"(c2[3]), "v"(c2[4]), "v"(c2[5]), "v"(c2[6]), "v"(c2[7]),
+          "v"(c2[8]), "v"(c2[9]), "v"(c2[10]), "v"(c2[11]), "v"(c2[12]), "v"(c2[13]), "v"(c2[14]), "v"(c2[15]),
+          "v"(c3[0]), "v"(c3[1]), "v"(c3[2]), "v"(c3[3]), "v"(c3[4]), "v"(c3[5]), "v"(c3[6]), "v"(c3[7]),
+          "v"(c3[8]), "v"(c3[9]), "v"(c3[10]), "v"(c3[11]), "v"(c3[12]), "v"(c3[13]), "v"(c3[14]), "v"(c3[15]),
+          "v"(t0), "v"(t1), "v"(t2), "v"(t3));
+}
 __device__ __forceinline__ void relu_clamp_bf16_x1(const f32x16 &c, u32x4 (&k)[2]) {
     const uint32_t t0 = __float_as_uint(c[0]) & 1u;
     asm(NR_CVC(0, 8, 9) NR_CVC(1, 10, 11) NR_CVC(2, 12, 13) NR_CVC(3, 14, 15)
@@ -331,7 +364,8 @@ __device__ __forceinline__ void relu_pack_tiles(const f32x16 (&acc)[NT], typenam
     typedef typename Lowp<PREC>::v8 v8;
     if constexpr (CL && PREC == NR_PRECISION_BF16) {
         u32x4 u[NT][2];
-        if constexpr (NT == 2) relu_clamp_bf16_x2(acc[0], acc[1], u);
+        if constexpr (NT == 4) relu_clamp_bf16_x4(acc[0], acc[1], acc[2], acc[3], u);
+        else if constexpr (NT == 2) relu_clamp_bf16_x2(acc[0], acc[1], u);
         else relu_clamp_bf16_x1(acc[0], u[0]);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -474,6 +508,81 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
         z1 = __uint_as_float(r[1]);
     }
     return (z0 + z1) + bf;
+}
+
+// The 128-point form of mlp32_lowp_nt for the stand-alone MLP (k_mlp16): two points per lane
+// (set s = 0, 1: point p of set s in lane p), four 32-point tiles (2s, 2s + 1).  Same
+// arithmetic per point, bit for bit; what changes is that every layer's operands -- two
+// ds_read_b128 of A operands and four of bias per wave -- serve four tiles instead of two.
+// At two tiles those reads kept the CU's LDS array ~80 % busy beside the MFMAs (49 ds_read_b128
+// per 64 points against 30 MFMAs: 196 LDS-array cycles per 960 MFMA cycles on each of the 4
+// SIMDs, MI355X_MICROARCH.md section LDS), and a layer's four independent MFMA chains give the
+// wave's own conversions more to overlap with.
+template <int PREC, int NH, bool CL>
+__device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                               int nh_rt, const float (&fr)[2], const float (&x)[2],
+                                               const float (&y)[2], const float (&z)[2], float (&out)[2]) {
+    typedef typename Lowp<PREC>::v8 v8;
+    const int nh = NH > 0 ? NH : nh_rt;
+    const int lane = lane_id(), h = lane >> 5;
+    f32x16 acc[4];
+    {
+        const v8 A = reinterpret_cast<const v8 *>(lp)[lane];
+        const f32x16 b0 = load_bias16(fl + 16 * h);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            // layer 0 of set s exactly as mlp32_lowp_nt's (see there)
+            const uint32_t p0 = cvt2<PREC>(x[s], y[s]);
+            const float dx = x[s] - lo16f<PREC>(p0), dy = y[s] - hi16f<PREC>(p0);
+            const uint32_t q = cvt2<PREC>(z[s], dx);
+            const uint32_t r = cvt2<PREC>(dy, z[s] - lo16f<PREC>(q));
+            uint32_t f = 0;
+            if (in0 == 4) {
+                const uint32_t f0 = cvt2<PREC>(fr[s], 0.0f);
+                f = cvt2<PREC>(fr[s], fr[s] - lo16f<PREC>(f0));
+            }
+            const uint32_t qf = (q & 0xffffu) | (f << 16);
+            const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
+            const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
+            const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
+            const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                acc[2 * s + t] = mfma32<PREC>(A, __builtin_bit_cast(v8, (u32x4){w0[t], w1[t], w2[t], w3[t]}), b0);
+        }
+    }
+    hidden_layers<PREC, 4, NH, CL>(lp, fl, nh, acc);
+    const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(nh));
+    const u32x4 wf[2] = {F4[h], F4[2 + h]};
+    const float bf = fl[32 + 32 * nh];
+    v8 k[4][2];
+    relu_pack_tiles<PREC, 4, CL>(acc, k);
+    float zt[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        float a = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            const u32x4 kv = __builtin_bit_cast(u32x4, k[t][st]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a = dot2<PREC>(kv[q], wf[st][q], a);
+        }
+        zt[t] = a;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[2 * s]), __float_as_uint(zt[2 * s + 1]), false,
+                                                        false);
+        out[s] = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + bf;
+    }
+}
+
+template <int PREC, bool CL>
+__device__ __forceinline__ void mlp128_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
+                                               int nh, const float (&fr)[2], const float (&x)[2], const float (&y)[2],
+                                               const float (&z)[2], float (&out)[2]) {
+    if (nh == 7) mlp32_lowp_128<PREC, 7, CL>(lp, fl, in0, nh, fr, x, y, z, out);
+    else mlp32_lowp_128<PREC, 0, CL>(lp, fl, in0, nh, fr, x, y, z, out);
 }
 
 template <int PREC, bool CL>

@@ -493,12 +493,17 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 #ifndef NR_MLP16_WPS_X3
 #define NR_MLP16_WPS_X3 4
 #endif
+// bf16 / fp16: the 128-point form holds four accumulators (64 VGPRs) and their operands
+#ifndef NR_MLP16_WPS_LP
+#define NR_MLP16_WPS_LP 3
+#endif
 // Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
 // matrix-core tiles: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks; the next
 // chunk's inputs are loaded before the current chunk's MLP, so their HBM latency (~2 us)
 // hides behind its MFMAs instead of stalling every wave once per chunk.
 template <int PREC>
-__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3 : NR_MLP16_WPS) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
+__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
+                                    : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     // the wave's chunk index is uniform: readfirstlane keeps the loop control (base, rem,
@@ -513,6 +518,42 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3 
             if (M.in0 == 4) f = p[3];
         }
     };
+    if constexpr (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16) {
+        // 128 points per wave and chunk (nr_mlp16.h mlp32_lowp_128): point base + lane and
+        // base + 64 + lane; a last chunk of at most 64 points takes the 64-point form
+        const long stride2 = 2 * stride;
+        long base = wave * 128;
+        float nx[2], ny[2], nz[2], nf[2];
+        load(base + lane, nx[0], ny[0], nz[0], nf[0]);
+        load(base + 64 + lane, nx[1], ny[1], nz[1], nf[1]);
+        for (; base < n; base += stride2) {
+            base = (long)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)base));  // uniform: SGPRs
+            const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
+            load(base + stride2 + lane, nx[0], ny[0], nz[0], nf[0]);
+            load(base + stride2 + 64 + lane, nx[1], ny[1], nz[1], nf[1]);
+            const long rem = n - base;
+            const bool ok0 = __builtin_fabsf(x[0]) <= LP_INPUT_BOUND && __builtin_fabsf(y[0]) <= LP_INPUT_BOUND &&
+                             __builtin_fabsf(z[0]) <= LP_INPUT_BOUND && __builtin_fabsf(f[0]) <= LP_INPUT_BOUND;
+            const bool ok1 = __builtin_fabsf(x[1]) <= LP_INPUT_BOUND && __builtin_fabsf(y[1]) <= LP_INPUT_BOUND &&
+                             __builtin_fabsf(z[1]) <= LP_INPUT_BOUND && __builtin_fabsf(f[1]) <= LP_INPUT_BOUND;
+            if (rem <= 64) {
+                const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
+                const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f[0], x[0], y[0], z[0], tmask,
+                                      M.lp_clamp && __ballot(!ok0) == 0);
+                if (lane < rem) Y[base + lane] = v;
+                continue;
+            }
+            float v[2];
+            if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!(ok0 && ok1)) == 0)
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, M.in0, M.nh, f, x, y, z, v);
+            else
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, M.in0, M.nh, f, x, y, z, v);
+            Y[base + lane] = v[0];
+            if (64 + lane < rem) Y[base + 64 + lane] = v[1];
+        }
+        return;
+    }
     long base = wave * 64;
     float nx, ny, nz, nf;
     load(base + lane, nx, ny, nz, nf);

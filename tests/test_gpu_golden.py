@@ -1,10 +1,11 @@
 """The HIP path against the reference's own renders (neuralGeometries/<g>.h5.ppm, 1024^2): their
 foreground masks (tests/golden/silhouettes.npz, made by make_golden.py) pin coverage.  The
 renders used the pure-neural scene (sceneSDF -> tanh(nSDF), volumeRender_kernel.cu:229) at the
-cameras recovered in SURVEY.md App. A; the GPU renders that scene at those cameras, full size,
-with the reference's MAX_STEPS (6000), in every precision, and must cover the same pixels as
-the reference's render to the IoU the restatement reaches (SURVEY: 0.962 plane_1 at 1024^2,
-0.895 car_1 at 128^2; test_oracle.py checks the CPU oracle at 256^2 / 128^2)."""
+cameras recovered for them (conftest.REF_CAMERAS, refined by tools/camera_fit.py); the GPU renders
+that scene at those cameras, full size, with the reference's MAX_STEPS (6000), in every precision,
+and must cover the same pixels as the reference's render: the oracle's fp32 frame differs from
+it in 40 (plane_1) and 16 (car_1) pixels of ~48 k / 128 k foreground ones.  (The renders'
+colours predate v1's shading and pin nothing: profiles/r3_shading_search.txt.)"""
 import json
 import os
 
@@ -12,11 +13,12 @@ import numpy as np
 import pytest
 
 import cudaneuralrender_amd as nr
-from conftest import REPO
+from conftest import REF_CAMERAS, REPO
 
 pytestmark = pytest.mark.gpu
 
-MIN_IOU = {"plane_1": 0.96, "car_1": 0.89}
+# fp32 / fp32x3 reach 0.9991 / 0.9998; the 16-bit MLPs move a few silhouette rays more
+MIN_IOU = {"plane_1": 0.996, "car_1": 0.998}
 RESULTS = []
 
 
@@ -39,7 +41,7 @@ def record():
 @pytest.mark.parametrize("name", ["plane_1", "car_1"])
 def test_gpu_silhouette_vs_reference_render(golden, name, prec):
     gold = _sil(golden, name)
-    rx, ry, zoom = (float(v) for v in golden["sil"][f"{name}/camera"])
+    rx, ry, zoom = REF_CAMERAS[name]
     iv, nm = nr.camera(rx, ry, zoom)
     with nr.Renderer(0) as r:
         r.load_h5(nr.geometry_path(name)).set_precision(prec)

@@ -47,7 +47,8 @@ def read_ppm(path):
     return np.frombuffer(data, np.uint8, w * h * 3, pos + 1).reshape(h, w, 3)
 
 
-CASES = {"plane_1": ("skin-matcap", (-18.3, 150.7, 2.25)), "car_1": ("Car Paint Red", (-79.0, 229.0, 3.05))}
+# cameras: refined from SURVEY App. A by maximising the silhouette IoU (tools/camera_fit.py)
+CASES = {"plane_1": ("skin-matcap", (-18.8021, 149.7984, 2.2702)), "car_1": ("Car Paint Red", (80.047, 140.0488, 3.1031))}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--res", type=int, default=256)
@@ -103,7 +104,9 @@ for name, (mc, (rx, ry, zoom)) in CASES.items():
         return exact, near.mean()
 
     res = []
-    for space, vec in (("view", ne), ("world", nw)):
+    nt = nw @ N  # the transpose of the normal matrix applied (rows: N^T n)
+    nt /= np.linalg.norm(nt, axis=1, keepdims=True)
+    for space, vec in (("view", ne), ("world", nw), ("viewT", nt)):
         for (cu, cv) in itertools.permutations(range(3), 2):
             for fu, fv in itertools.product((False, True), repeat=2):
                 u = vec[:, cu] * 0.5 + 0.5
@@ -112,6 +115,27 @@ for name, (mc, (rx, ry, zoom)) in CASES.items():
                 v = 1 - v if fv else v
                 e, n_ = score(u, v)
                 res.append((n_, e, f"{space:5s} u={'-' if fu else '+'}{'xyz'[cu]} v={'-' if fv else '+'}{'xyz'[cv]}"))
+    # sphere-map variants on the reflected view ray (camera space: the eye looks down -z; the
+    # pixel's direction normalize(u, v, -2), initMarcher :315-320): r = d - 2 (d . n) n,
+    # m = 2 sqrt(r.x^2 + r.y^2 + (r.z + 1)^2), uv = r.xy / m + 1/2 (flips included)
+    yy, xx = np.nonzero(both)
+    du = xx / a.res * 2 - 1
+    dv = yy / a.res * 2 - 1
+    dc = np.stack([du, dv, -2 * np.ones_like(du)], -1)
+    dc /= np.linalg.norm(dc, axis=1, keepdims=True)
+    for zs in (1, -1):
+        r_ = dc - 2 * (dc * ne).sum(1, keepdims=True) * ne
+        m = 2 * np.sqrt(r_[:, 0] ** 2 + r_[:, 1] ** 2 + (r_[:, 2] + zs) ** 2)
+        for fu, fv in itertools.product((False, True), repeat=2):
+            for sw in (False, True):
+                u, v = r_[:, 0] / m + 0.5, r_[:, 1] / m + 0.5
+                if sw:
+                    u, v = v, u
+                u = 1 - u if fu else u
+                v = 1 - v if fv else v
+                e, n_ = score(u, v)
+                res.append((n_, e, f"spheremap(z{'+' if zs > 0 else '-'}1) {'swap ' if sw else ''}"
+                                   f"u{'-' if fu else '+'} v{'-' if fv else '+'}"))
     res.sort(reverse=True)
     for n_, e, lab in res[:8]:
         print(f"   {lab}: exact {e:.4f}  within {a.radius} texels {n_:.4f}")
