@@ -64,10 +64,8 @@ NR_HD constexpr inline int lp32_floats(int nh) { return 32 + 32 * nh + 4; }
 // activation at or below 1/4 (interval bounds, nr_pack.cpp pack_lowp_32)
 constexpr float LP_INPUT_BOUND = 1048576.0f;
 // fp32 clamped-ReLU pack (pack_fp32_16): inputs within +-F32_INPUT_BOUND keep every scaled
-// activation at or below 1/2, and inputs of magnitude below F32_INPUT_TINY (other than 0)
-// take the max-ReLU form too (nr_mlp16.h inputs_in_bound_f32)
+// activation at or below 1/2 (nr_mlp16.h inputs_in_bound_f32; beyond it the add + max form)
 constexpr float F32_INPUT_BOUND = 1024.0f;
-constexpr float F32_INPUT_TINY = 0x1p-60f;
 
 // fp32x3 pack (pack_x3_32): fp32-class hidden layers on the fp16 matrix core by a three-term
 // split, a.w ~ ah.wh + al.wh + ah.wl (nr_mlp16.h mlp32_x3_nt).  16-bit elements (fp16):

@@ -252,10 +252,10 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 
 // registers 8s..8s+7 of an accumulator -> ReLU'd 16-bit B operand of k-step s:
 // v_cvt_pk rounds pairs (RNE), v_pk_max_i16 against 0 is the ReLU on the 16-bit patterns
-// (negative values and -0 have the sign bit set).  (The VOP3 clamp bit of v_cvt_pk would
-// fold the ReLU into the conversion for activations pre-scaled below 1 --
-// tools/cvt_clamp_probe.hip -- but the compiler inserts no MFMA->VALU wait states before
-// inline asm, and no builtin exposes the bit.)
+// (negative values and -0 have the sign bit set).  (bf16 on the clamped pack folds the ReLU into
+// the conversion: relu_clamp_bf16_x* below.  For fp16 hipcc would fold min(max(cvt(x), 0), 1)
+// into v_cvt_pk_f16_f32 ... clamp, but the scaled pack that needs costs fp16 its precision:
+// nr_pack.cpp pack_lowp_32.)
 template <int PREC>
 __device__ __forceinline__ typename Lowp<PREC>::v8 relu_pack8(const f32x16 &c, int s) {
     typedef typename Lowp<PREC>::e e16;

@@ -66,27 +66,41 @@ float fp16f(uint16_t h) {
 // activation, for network inputs within +-bound, is at most 2^e[l] / 2^margin.  Interval
 // arithmetic in double over the exact f32 weights; the margin covers the rounding of the
 // evaluation (bf16: 2 -- weights and activations rounded to bf16, relative 2^-9 each per
-// layer, ~3% over 8 layers; fp32: 1 -- f32 chains, ~2^-19 relative).  Returns false when a
-// scale or a scaled weight would leave the range where power-of-two scaling is exact.
+// layer, ~3% over 8 layers; fp32: 1 -- f32 chains, ~2^-19 relative).  The rounding error of a
+// unit is relative to the sum of its terms' magnitudes S = |b| + sum |w| max(|lo|, |hi|), not to
+// its value, so a unit whose bias cancels large products could round past the interval bound:
+// the bound used is top + eps S (bf16 eps 2^-6, fp32 2^-19).  Returns false -- the
+// unscaled pack, ReLU by max -- when a scale or a scaled weight would leave the range where
+// power-of-two scaling is exact, or a nonzero weight or bias is below 2^-60 in magnitude (with
+// such values the scaled chains could round differently from the unscaled ones near f32's
+// subnormal range).
 static bool clamp_scales(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
-                         const std::vector<std::vector<float>> &B, std::vector<int> &e, double bound, int margin) {
+                         const std::vector<std::vector<float>> &B, std::vector<int> &e, double bound, int margin,
+                         double eps) {
     const int nl = (int)dims.size() - 1;
     std::vector<double> lo(dims[0], -bound), hi(dims[0], bound);
     e.assign(nl - 1, 0);
+    for (int l = 0; l < nl; ++l) {
+        for (float w : K[l])
+            if (w != 0.0f && std::fabs(w) < 0x1p-60f) return false;
+        for (float b : B[l])
+            if (b != 0.0f && std::fabs(b) < 0x1p-60f) return false;
+    }
     for (int l = 0; l < nl - 1; ++l) {
         const int in = dims[l], out = dims[l + 1];
         std::vector<double> nlo(out), nhi(out);
         double top = 0.0;
         for (int u = 0; u < out; ++u) {
-            double a = B[l][u], b = B[l][u];
+            double a = B[l][u], b = B[l][u], S = std::fabs((double)B[l][u]);
             for (int i = 0; i < in; ++i) {
                 const double w = K[l][(size_t)i * out + u];
                 a += std::min(w * lo[i], w * hi[i]);
                 b += std::max(w * lo[i], w * hi[i]);
+                S += std::fabs(w) * std::max(std::fabs(lo[i]), std::fabs(hi[i]));
             }
             nlo[u] = std::max(a, 0.0);  // ReLU
             nhi[u] = std::max(b, 0.0);
-            top = std::max(top, nhi[u]);
+            top = std::max(top, nhi[u] + eps * S);
         }
         if (!std::isfinite(top)) return false;
         e[l] = top > 0.0 ? (int)std::ceil(std::log2(top)) + margin : 0;
@@ -106,6 +120,51 @@ static bool clamp_scales(const std::vector<int> &dims, const std::vector<std::ve
                 return false;
     }
     return true;
+}
+
+// Hard bounds on every ReLU layer's largest activation for xyz inputs within +-xyz_b (and a 4th
+// input within +-f_b): the maximum of the interval bounds (double, over the exact f32 weights)
+// over a grid of sub-boxes of the input box -- 16 per xyz axis; 8 per axis x 16 frame slabs for
+// a 4th input.  Still a hard bound, 2-4 binades tighter than one interval pass over the whole box
+// on the bundled networks (interval arithmetic ignores the correlation of a unit's inputs, and a
+// small box leaves less of it).  Returns false on a non-finite bound.
+static bool box_tops(const std::vector<int> &dims, const std::vector<std::vector<float>> &K,
+                     const std::vector<std::vector<float>> &B, double xyz_b, double f_b, std::vector<double> &top) {
+    const int nl = (int)dims.size() - 1, in0 = dims[0];
+    const int mx = in0 == 4 ? 8 : 16, mf = in0 == 4 ? 16 : 1;
+    bool ok = true;
+    std::vector<double> lo, hi, nlo, nhi;
+    top.assign(nl - 1, 0.0);
+    for (int box = 0; box < mx * mx * mx * mf && ok; ++box) {
+        lo.assign(in0, 0.0);
+        hi.assign(in0, 0.0);
+        for (int i = 0; i < in0; ++i) {
+            const int m = i < 3 ? mx : mf, k = i < 3 ? (box / (i == 0 ? 1 : i == 1 ? mx : mx * mx)) % mx : box / (mx * mx * mx);
+            const double b = i < 3 ? xyz_b : f_b;
+            lo[i] = -b + 2.0 * b * k / m;
+            hi[i] = k + 1 == m ? b : -b + 2.0 * b * (k + 1) / m;
+        }
+        for (int l = 0; l < nl - 1; ++l) {
+            const int in = dims[l], out = dims[l + 1];
+            nlo.assign(out, 0.0);
+            nhi.assign(out, 0.0);
+            for (int u = 0; u < out; ++u) {
+                double a = B[l][u], b = B[l][u];
+                for (int i = 0; i < in; ++i) {
+                    const double w = K[l][(size_t)i * out + u];
+                    a += std::min(w * lo[i], w * hi[i]);
+                    b += std::max(w * lo[i], w * hi[i]);
+                }
+                if (!std::isfinite(a) || !std::isfinite(b)) ok = false;
+                nlo[u] = std::max(a, 0.0);
+                nhi[u] = std::max(b, 0.0);
+                top[l] = std::max(top[l], nhi[u]);
+            }
+            lo.swap(nlo);
+            hi.swap(nhi);
+        }
+    }
+    return ok;
 }
 
 // Layer l's weights times 2^(e[l-1] - e[l]) and its bias times 2^-e[l] (e[-1] = 0, e[last]
@@ -133,16 +192,20 @@ inline int unit16(int g, int k, bool final_consumer) { return final_consumer ? 8
 // (rounding is scale-invariant while values stay normal), so the network's output is the
 // unscaled network's bit for bit, and ReLU activations stay <= 1/2 for inputs within the
 // bound -- v_add_f32 with the clamp bit is then the bias add and the ReLU in one
-// instruction (nr_mlp16.h).  (An intermediate value of the unscaled network below
-// 2^(e - 126) in magnitude, e <= ~27 for the bundled networks, would round differently
-// once scaled; nonzero values of a bounded-input network sit at the bias/weight scale,
-// ~1e-10 and above, and the kernels send inputs below F32_INPUT_TINY to the max form.)
+// instruction (nr_mlp16.h).  A wave with an input beyond the bound runs the add + max form on
+// the same pack: larger inputs make larger scaled values, still exact.  Precondition of the
+// "bit for bit": no fmaf result of the unscaled evaluation lies in (0, 2^(e - 126)) in magnitude
+// (e <= ~27 for the bundled networks: below ~10^-30), where the scaled evaluation would round a
+// subnormal.  Sums that cancel are exact (Sterbenz), so such a result needs tiny operands:
+// clamp_scales refuses networks with nonzero weights or biases below 2^-60, and inputs that
+// small (tests/test_gpu_f32_clamp.py drives 1e-25) only reach it through a layer-0 unit whose
+// bias is exactly 0 and whose products are all below ~2^-100.
 bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<float>> &Kin,
                   const std::vector<std::vector<float>> &Bin, std::vector<float> &pack, int *clamp) {
     if (!fused_shape_ok(dims)) return false;
     int nl = (int)dims.size() - 1, nh = nl - 2, in0 = dims[0];
     std::vector<int> e;
-    const bool cl = clamp_scales(dims, Kin, Bin, e, (double)F32_INPUT_BOUND, 1);
+    const bool cl = clamp_scales(dims, Kin, Bin, e, (double)F32_INPUT_BOUND, 1, 0x1p-19);
     if (clamp) *clamp = cl ? 1 : 0;
     std::vector<std::vector<float>> K(Kin), B(Bin);
     if (cl) {
@@ -197,8 +260,12 @@ bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<fl
     // e[last] = 0), so activations come out scaled by 2^-e[l] and the last layer's output is
     // unscaled: power-of-two scaling is exact in bf16 and f32, so the network computes the same
     // values as unscaled, and activations stay below 1 for the clamped ReLU (nr_mlp16.h)
+    // (fp16 stays unscaled: its narrow exponent range turns the scaled activations -- held below
+    // 1 by a hard interval bound that sits 7-10 binades above the actual values -- into
+    // subnormals; measured round 3: +10 % MLP rate, C5 crops' coverage IoU vs the fp32 oracle
+    // 0.98 -> 0.74-0.86.  DESIGN.md section 2.)
     std::vector<int> e;
-    const bool cl = bf && clamp_scales(dims, Kin, Bin, e, (double)LP_INPUT_BOUND, 2);
+    const bool cl = bf && clamp_scales(dims, Kin, Bin, e, (double)LP_INPUT_BOUND, 2, 0x1p-6);
     if (clamp) *clamp = cl ? 1 : 0;
     std::vector<std::vector<float>> K(Kin), B(Bin);
     if (cl) apply_scales(e, K, B);
@@ -267,44 +334,12 @@ bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<floa
     bool ok = true;
     std::vector<int> e(nl - 1, 0);
     {
-        // The bound is the maximum of the interval bounds over a grid of sub-boxes of the input
-        // box (16 per xyz axis; 8 per axis x 16 frame slabs for a 4th input): still a hard bound,
-        // 2-4 binades tighter than one interval pass over the whole box on the bundled networks.
-        // Activations then sit higher in the window below 2^10, so fewer residuals al = a - ah
-        // fall into fp16's subnormal range, which would cost them relative precision (emulated:
-        // mean error vs fp64 from 2.4-3.9x to 1.8-2.4x the f32 chain's, a random 4-input
-        // network 5.8x -> 3.1x; tests/test_gpu_fp32x3.py).
-        const int mx = in0 == 4 ? 8 : 16, mf = in0 == 4 ? 16 : 1;
-        std::vector<double> top(nl - 1, 0.0), lo, hi, nlo, nhi;
-        for (int box = 0; box < mx * mx * mx * mf && ok; ++box) {
-            lo.assign(in0, 0.0);
-            hi.assign(in0, 0.0);
-            for (int i = 0; i < in0; ++i) {
-                const int m = i < 3 ? mx : mf, k = i < 3 ? (box / (i == 0 ? 1 : i == 1 ? mx : mx * mx)) % mx : box / (mx * mx * mx);
-                const double b = i < 3 ? (double)X3_INPUT_BOUND : (double)X3_FRAME_BOUND;
-                lo[i] = -b + 2.0 * b * k / m;
-                hi[i] = k + 1 == m ? b : -b + 2.0 * b * (k + 1) / m;
-            }
-            for (int l = 0; l < nl - 1; ++l) {
-                const int in = dims[l], out = dims[l + 1];
-                nlo.assign(out, 0.0);
-                nhi.assign(out, 0.0);
-                for (int u = 0; u < out; ++u) {
-                    double a = B[l][u], b = B[l][u];
-                    for (int i = 0; i < in; ++i) {
-                        const double w = K[l][(size_t)i * out + u];
-                        a += std::min(w * lo[i], w * hi[i]);
-                        b += std::max(w * lo[i], w * hi[i]);
-                    }
-                    if (!std::isfinite(a) || !std::isfinite(b)) ok = false;
-                    nlo[u] = std::max(a, 0.0);
-                    nhi[u] = std::max(b, 0.0);
-                    top[l] = std::max(top[l], nhi[u]);
-                }
-                lo.swap(nlo);
-                hi.swap(nhi);
-            }
-        }
+        // the scales from the sub-box interval bounds (box_tops): activations sit higher in the
+        // window below 2^10, so fewer residuals al = a - ah fall into fp16's subnormal range,
+        // which would cost them relative precision (emulated: mean error vs fp64 from 2.4-3.9x to
+        // 1.8-2.4x the f32 chain's, a random 4-input network 5.8x -> 3.1x; tests/test_gpu_fp32x3.py)
+        std::vector<double> top;
+        ok = box_tops(dims, K, B, (double)X3_INPUT_BOUND, (double)X3_FRAME_BOUND, top);
         for (int l = 0; l < nl - 1 && ok; ++l) {
             if (!std::isfinite(top[l])) ok = false;
             e[l] = top[l] > 0.0 ? (int)std::ceil(std::log2(top[l])) - 10 : 0;

@@ -498,75 +498,90 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 #define NR_MLP16_WPS_LP 3
 #endif
 // Stand-alone batched MLP (NeuralNetwork::forward, neuralNetwork.cpp:54-63) on the
-// matrix-core tiles: X [n][in0] -> Y [n].  Grid-stride over 64-point chunks; the next
-// chunk's inputs are loaded before the current chunk's MLP, so their HBM latency (~2 us)
-// hides behind its MFMAs instead of stalling every wave once per chunk.
-template <int PREC>
+// matrix-core tiles: X [n][in0] -> Y [n], n < 2^26 per launch (launch_mlp16 splits).
+// Grid-stride over chunks of 64 points (fp32, fp32x3) or 128 points (bf16, fp16: two per lane,
+// nr_mlp16.h mlp32_lowp_128).  The inputs and outputs go through buffer resources sized to the
+// arrays: a position past the end loads zeros and drops its store, so every load and store is
+// unconditional -- the next chunk's inputs are requested before the current chunk's MLP and
+// waited for only after it (a load behind a lane-divergent branch was waited for at once,
+// stalling every wave ~1 us per chunk), and the per-lane offsets are 32-bit.
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_of(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+// IN0: the network's inputs (3, or 4 with the frame): a template parameter, so that the load is
+// not behind a branch (whose join waited for it)
+template <int PREC, int IN0>
 __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
-                                    : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, long n) {
+                                    : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, int n) {
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
-    // the wave's chunk index is uniform: readfirstlane keeps the loop control (base, rem,
-    // tmask) in SGPRs instead of 64-bit VALU arithmetic on every lane
-    const long wave = (long)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const long stride = (((long)gridDim.x * blockDim.x) >> 6) * 64;
-    auto load = [&](long i, float &x, float &y, float &z, float &f) {
-        x = y = z = f = 0.0f;
-        if (i < n) {
-            const float *p = X + i * M.in0;
-            x = p[0]; y = p[1]; z = p[2];
-            if (M.in0 == 4) f = p[3];
+    constexpr int in0 = IN0;
+    M.in0 = IN0;
+    const auto rx = buffer_of(X, (uint32_t)n * (uint32_t)in0 * 4u), ry = buffer_of(Y, (uint32_t)n * 4u);
+    // point i's inputs (zeros past the end); the 4th is the frame for 4-input networks
+    auto load = [&](uint32_t i, float &x, float &y, float &z, float &f) {
+        if constexpr (in0 == 4) {
+            const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rx, i * 16u, 0, 0);
+            x = __uint_as_float(v.x); y = __uint_as_float(v.y); z = __uint_as_float(v.z); f = __uint_as_float(v.w);
+        } else {
+            const u32x3v v = __builtin_amdgcn_raw_buffer_load_b96(rx, i * 12u, 0, 0);
+            x = __uint_as_float(v.x); y = __uint_as_float(v.y); z = __uint_as_float(v.z); f = 0.0f;
         }
     };
+    auto store = [&](uint32_t i, float v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, i * 4u, 0, 0); };
+    // the wave's chunk index is uniform (SGPRs)
+    const int wave = (int)blockIdx.x * (int)(blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int waves = (int)gridDim.x * (int)(blockDim.x >> 6);
     if constexpr (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16) {
-        // 128 points per wave and chunk (nr_mlp16.h mlp32_lowp_128): point base + lane and
-        // base + 64 + lane; a last chunk of at most 64 points takes the 64-point form
-        const long stride2 = 2 * stride;
-        long base = wave * 128;
+        // 128 points per wave and chunk: point base + lane and base + 64 + lane; a last chunk of
+        // at most 64 points takes the 64-point form
+        const int stride2 = waves * 128;
         float nx[2], ny[2], nz[2], nf[2];
-        load(base + lane, nx[0], ny[0], nz[0], nf[0]);
-        load(base + 64 + lane, nx[1], ny[1], nz[1], nf[1]);
+        int base = wave * 128;
+        load((uint32_t)(base + lane), nx[0], ny[0], nz[0], nf[0]);
+        load((uint32_t)(base + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
         for (; base < n; base += stride2) {
-            base = (long)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)base));  // uniform: SGPRs
+            base = __builtin_amdgcn_readfirstlane(base);  // uniform: SGPRs, scalar branches
             const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
-            load(base + stride2 + lane, nx[0], ny[0], nz[0], nf[0]);
-            load(base + stride2 + 64 + lane, nx[1], ny[1], nz[1], nf[1]);
-            const long rem = n - base;
-            const bool ok0 = __builtin_fabsf(x[0]) <= LP_INPUT_BOUND && __builtin_fabsf(y[0]) <= LP_INPUT_BOUND &&
-                             __builtin_fabsf(z[0]) <= LP_INPUT_BOUND && __builtin_fabsf(f[0]) <= LP_INPUT_BOUND;
-            const bool ok1 = __builtin_fabsf(x[1]) <= LP_INPUT_BOUND && __builtin_fabsf(y[1]) <= LP_INPUT_BOUND &&
-                             __builtin_fabsf(z[1]) <= LP_INPUT_BOUND && __builtin_fabsf(f[1]) <= LP_INPUT_BOUND;
+            load((uint32_t)(base + stride2 + lane), nx[0], ny[0], nz[0], nf[0]);
+            load((uint32_t)(base + stride2 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+            const int rem = n - base;
+            // the bf16 clamped pack's input bound (NaN is not within it)
+            constexpr float XB = LP_INPUT_BOUND, FB = LP_INPUT_BOUND;
+            const bool ok0 = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
+                             __builtin_fabsf(f[0]) <= FB;
+            const bool ok1 = __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB && __builtin_fabsf(z[1]) <= XB &&
+                             __builtin_fabsf(f[1]) <= FB;
             if (rem <= 64) {
                 const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
-                const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f[0], x[0], y[0], z[0], tmask,
-                                      M.lp_clamp && __ballot(!ok0) == 0);
-                if (lane < rem) Y[base + lane] = v;
+                store((uint32_t)(base + lane), mlp16(M, S.s32, S.slp, S.sfl, PREC, f[0], x[0], y[0], z[0], tmask,
+                                                     M.lp_clamp && __ballot(!ok0) == 0));
                 continue;
             }
             float v[2];
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!(ok0 && ok1)) == 0)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, M.in0, M.nh, f, x, y, z, v);
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v);
             else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, M.in0, M.nh, f, x, y, z, v);
-            Y[base + lane] = v[0];
-            if (64 + lane < rem) Y[base + 64 + lane] = v[1];
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v);
+            store((uint32_t)(base + lane), v[0]);
+            store((uint32_t)(base + 64 + lane), v[1]);
         }
         return;
     }
-    long base = wave * 64;
+    const int stride = waves * 64;
+    int base = wave * 64;
     float nx, ny, nz, nf;
-    load(base + lane, nx, ny, nz, nf);
+    load((uint32_t)(base + lane), nx, ny, nz, nf);
     for (; base < n; base += stride) {
-        base = (long)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(base >> 32)) << 32) |
-                      (uint32_t)__builtin_amdgcn_readfirstlane((int)base));  // uniform: SGPRs
-        const long i = base + lane;
+        base = __builtin_amdgcn_readfirstlane(base);
         const float x = nx, y = ny, z = nz, f = nf;
-        load(base + stride + lane, nx, ny, nz, nf);
-        const long rem = n - base;
+        load((uint32_t)(base + stride + lane), nx, ny, nz, nf);
+        const int rem = n - base;
         const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
-        const float v = mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask, M.lp_clamp && inputs_in_bound(x, y, z, f));
-        if (i < n) Y[i] = v;
+        store((uint32_t)(base + lane),
+              mlp16(M, S.s32, S.slp, S.sfl, PREC, f, x, y, z, tmask, M.lp_clamp && inputs_in_bound(x, y, z, f)));
     }
 }
 
@@ -611,15 +626,23 @@ hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int
 
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
     const int sm = smem16_bytes(M, prec, false);
-    if (prec == NR_PRECISION_BF16)
-        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
-    else if (prec == NR_PRECISION_FP16)
-        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
-    else if (prec == NR_PRECISION_FP32X3)
-        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP32X3>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
-    else
-        hipLaunchKernelGGL(k_mlp16<NR_PRECISION_FP32>, dim3(grid), dim3(256), sm, st, M, X, Y, n);
-    return hipGetLastError();
+    // segments of at most 2^26 points: the kernel's buffer offsets (n * in0 * 4 bytes) are 32-bit
+    constexpr long SEG = 1l << 26;
+    for (long p0 = 0; p0 < n; p0 += SEG) {
+        const int m = (int)std::min(SEG, n - p0);
+        const float *x = X + p0 * M.in0;
+        float *y = Y + p0;
+        const int g = (int)std::min<long>(grid, ((long)m + 255) / 256);
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
+        const bool four = M.in0 == 4;
+        if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
+        else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
+        else if (prec == NR_PRECISION_FP32X3) four ? go(k_mlp16<NR_PRECISION_FP32X3, 4>) : go(k_mlp16<NR_PRECISION_FP32X3, 3>);
+        else four ? go(k_mlp16<NR_PRECISION_FP32, 4>) : go(k_mlp16<NR_PRECISION_FP32, 3>);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {

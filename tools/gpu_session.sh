@@ -4,7 +4,8 @@
 # its own time limit and the steps are chained, so the first failure ends the session.
 # usage (GPU box, repo root): bash tools/gpu_session.sh TAG [steps...]
 #   steps: smoke tests prof mlp cfg pmc_bf16 pmc_fp16 pmc_x3 march bench   (default: smoke tests prof mlp)
-#   env: PYTEST_EXTRA (extra pytest arguments, e.g. -k x3), BENCH_ARGS
+#   env: PYTEST_EXTRA (extra pytest arguments, no spaces inside one), PYTEST_K (a -k expression),
+#        BENCH_ARGS
 set -o pipefail
 TAG=${1:?tag}; shift
 STEPS=${*:-smoke tests prof mlp}
@@ -14,7 +15,7 @@ for s in $STEPS; do
     echo "[$(date +%T)] step $s" >&2
     case $s in
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 ;;
-    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=6 -v $PYTEST_EXTRA --timeout 300 --timeout-method thread > $O/gputests_$TAG.log 2>&1 ;;
+    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=6 -v $PYTEST_EXTRA ${PYTEST_K:+-k "$PYTEST_K"} --timeout 300 --timeout-method thread > $O/gputests_$TAG.log 2>&1 ;;
     prof) timeout -k 10 900 bash tools/profile_round.sh $TAG > $O/profile_round_$TAG.log 2>&1 ;;
     mlp) timeout -k 10 300 python -u tools/mlp_bench.py --n 16777216 --iters 10 --precision fp32,bf16,fp16,fp32x3 --bpc 4,8 > $O/mlp_$TAG.log 2>&1 ;;
     cfg) timeout -k 10 400 python -u tools/config_bench.py --frames 5 > $O/cfg_$TAG.log 2>&1 ;;
