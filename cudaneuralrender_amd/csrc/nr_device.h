@@ -190,6 +190,9 @@ __device__ __forceinline__ float sqrt_rn_normal(float x) {
     return rp > 0.0f ? sp : r;
 }
 
+#ifndef NR_SCENE_SCREEN
+#define NR_SCENE_SCREEN 1
+#endif
 __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
@@ -223,6 +226,33 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // ones), the short sequence gives the same bits as sqrtf.
     const float lo = fmaxf(zz, fmaxf(fminf(fminf(xx[0], xx[1]), xx[2]), fminf(fminf(yy[0], yy[1]), yy[2])));
     const float hi = (fmaxf(fmaxf(xx[0], xx[1]), xx[2]) + fmaxf(fmaxf(yy[0], yy[1]), yy[2])) + zz;
+#if NR_SCENE_SCREEN
+    // Screening (round 3): smoothUnion(s, d, k) with d - s >= k is fmaf(d, 0, s) -- it does not
+    // depend on d's value, only on that test (and on d's sign when s is +-0, where the test
+    // already makes d >= k > 0).  The running union never exceeds the surface value nsdf
+    // (smoothUnion(a, b) <= min(a, b)), so a sphere whose distance from the raw v_sqrt_f32 (within
+    // 1 ulp of the correctly rounded root; tools/sqrt_exhaustive.hip) is beyond nsdf + k by more
+    // than 2^-18 of the magnitudes involved (a thousand-fold margin over the rounding differences)
+    // is beyond the running value + k in every lane: when that holds for the whole wave, the
+    // sphere costs v_sqrt_f32 and the test instead of the correction, the sub and the union --
+    // bit for bit the same result.  Spheres that some lane is near take the exact path.
+    if (__ballot(!(lo >= 0x1p-96f && hi <= 0x1.fffffep127f)) == 0) {
+        float s = nsdf;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const float sa = __builtin_amdgcn_sqrtf(q[i]);
+            const float da = sa - 0.1f;
+            const bool far = da - nsdf >= 0.01f + (__builtin_fabsf(sa) + __builtin_fabsf(nsdf) + 0.01f) * 0x1p-18f;
+            if (__ballot(!far) == 0) s = __builtin_fmaf(da, 0.0f, s);
+            else s = smooth_union(s, sqrt_rn_normal(q[i]) - 0.1f, 0.01f);
+        }
+        return s;
+    }
+    float s = nsdf;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) s = smooth_union(s, sqrtf(q[i]) - 0.1f, 0.01f);
+    return s;
+#else
     if (__ballot(!(lo >= 0x1p-96f && hi <= 0x1.fffffep127f)) == 0) {
 #pragma unroll
         for (int i = 0; i < 9; ++i) d[i] = sqrt_rn_normal(q[i]) - 0.1f;
@@ -234,6 +264,7 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
 #pragma unroll
     for (int i = 0; i < 9; ++i) s = smooth_union(s, d[i], 0.01f);
     return s;
+#endif
 }
 
 // manySphere(p, nSDF, false) (:176-196): the 9 spheres smooth-subtracted from the surface,

@@ -518,6 +518,9 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
 // per 64 points against 30 MFMAs: 196 LDS-array cycles per 960 MFMA cycles on each of the 4
 // SIMDs, MI355X_MICROARCH.md section LDS), and a layer's four independent MFMA chains give the
 // wave's own conversions more to overlap with.
+#ifndef NR_LP_FINAL_MFMA
+#define NR_LP_FINAL_MFMA 0
+#endif
 template <int PREC, int NH, bool CL>
 __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh_rt, const float (&fr)[2], const float (&x)[2],
@@ -557,6 +560,25 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
     const float bf = fl[32 + 32 * nh];
     v8 k[4][2];
     relu_pack_tiles<PREC, 4, CL>(acc, k);
+#if NR_LP_FINAL_MFMA
+    // A/B: the final layer as 2 MFMAs per tile with the weights as row 0 of the A operand
+    // (lanes 0 and 32), the point's value in register 0 of lanes 0-31
+    const bool row0 = (lane & 31) == 0;
+    const v8 A0 = __builtin_bit_cast(v8, row0 ? wf[0] : (u32x4){0u, 0u, 0u, 0u});
+    const v8 A1 = __builtin_bit_cast(v8, row0 ? wf[1] : (u32x4){0u, 0u, 0u, 0u});
+    float zt[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const f32x16 zero = {};
+        zt[t] = mfma32<PREC>(A1, k[t][1], mfma32<PREC>(A0, k[t][0], zero))[0];
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[2 * s]), __float_as_uint(zt[2 * s + 1]), false,
+                                                        false);
+        out[s] = __uint_as_float(r[0]) + bf;
+    }
+#else
     float zt[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -575,6 +597,7 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
                                                         false);
         out[s] = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + bf;
     }
+#endif
 }
 
 template <int PREC, bool CL>
