@@ -312,13 +312,28 @@ __device__ __forceinline__ void relu_clamp_bf16_x2(const f32x16 &c, const f32x16
           "v"(d[8]), "v"(d[9]), "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15]),
           "v"(t0), "v"(t1));
 }
+// A/B (NR_LP_CVT_PRIO): raise the wave's issue priority over its conversion block, so that a
+// wave leaves the VALU-only phase sooner and the matrix pipe idles less while every wave of the
+// SIMD converts
+#ifndef NR_LP_CVT_PRIO
+#define NR_LP_CVT_PRIO 0
+#endif
+#if NR_LP_CVT_PRIO
+#define NR_CVT_PRIO_ON "s_setprio " NR_STR(NR_LP_CVT_PRIO) "\n"
+#define NR_CVT_PRIO_OFF "s_setprio 0\n"
+#define NR_STR2(x) #x
+#define NR_STR(x) NR_STR2(x)
+#else
+#define NR_CVT_PRIO_ON ""
+#define NR_CVT_PRIO_OFF ""
+#endif
 // four tiles (the 128-point MLP): one block, so that no MFMA of the next layer can be scheduled
 // between the conversions of two tile pairs while the pair not yet converted is read
 __device__ __forceinline__ void relu_clamp_bf16_x4(const f32x16 &c0, const f32x16 &c1, const f32x16 &c2, const f32x16 &c3,
                                                    u32x4 (&k)[4][2]) {
     const uint32_t t0 = __float_as_uint(c0[0]) & 1u, t1 = __float_as_uint(c1[0]) & 1u;  // the touches
     const uint32_t t2 = __float_as_uint(c2[0]) & 1u, t3 = __float_as_uint(c3[0]) & 1u;
-    asm(NR_CVC(0, 32, 33) NR_CVC(1, 34, 35) NR_CVC(2, 36, 37) NR_CVC(3, 38, 39)
+    asm(NR_CVT_PRIO_ON NR_CVC(0, 32, 33) NR_CVC(1, 34, 35) NR_CVC(2, 36, 37) NR_CVC(3, 38, 39)
          NR_CVC(4, 40, 41) NR_CVC(5, 42, 43) NR_CVC(6, 44, 45) NR_CVC(7, 46, 47)
          NR_CVC(8, 48, 49) NR_CVC(9, 50, 51) NR_CVC(10, 52, 53) NR_CVC(11, 54, 55)
          NR_CVC(12, 56, 57) NR_CVC(13, 58, 59) NR_CVC(14, 60, 61) NR_CVC(15, 62, 63)
@@ -326,7 +341,7 @@ __device__ __forceinline__ void relu_clamp_bf16_x4(const f32x16 &c0, const f32x1
          NR_CVC(20, 72, 73) NR_CVC(21, 74, 75) NR_CVC(22, 76, 77) NR_CVC(23, 78, 79)
          NR_CVC(24, 80, 81) NR_CVC(25, 82, 83) NR_CVC(26, 84, 85) NR_CVC(27, 86, 87)
          NR_CVC(28, 88, 89) NR_CVC(29, 90, 91) NR_CVC(30, 92, 93) NR_CVC(31, 94, 95)
-        "s_nop 1"
+        NR_CVT_PRIO_OFF "s_nop 1"
         : "=&v"(k[0][0][0]), "=&v"(k[0][0][1]), "=&v"(k[0][0][2]), "=&v"(k[0][0][3]),
           "=&v"(k[0][1][0]), "=&v"(k[0][1][1]), "=&v"(k[0][1][2]), "=&v"(k[0][1][3]),
           "=&v"(k[1][0][0]), "=&v"(k[1][0][1]), "=&v"(k[1][0][2]), "=&v"(k[1][0][3]),
