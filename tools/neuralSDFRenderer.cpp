@@ -4,7 +4,7 @@
 // and spin modes (:404-478), output naming (:445-461), PNG with the reference's
 // 180-degree rotation, and the throughput printf (:436-437).  The GLUT interactive
 // viewer (:480-519) needs a display and is not built; extra flags: --max-steps,
-// --precision {fp32,bf16,fp16}, --scene {v1,tanh}, --ppm (also write a .ppm).
+// --precision {fp32,bf16,fp16,fp32x3}, --scene {v1,tanh}, --ppm (also write a .ppm).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -53,7 +53,7 @@ static void usage() {
                  "\t--single render one frame and save it\n"
                  "\t--spin render 360 frames rotating about y\n"
                  "\t--animation 4-input networks (frame number as 4th input)\n"
-                 "\t--max-steps N (default 6000)  --precision fp32|bf16|fp16  --scene v1|tanh  --ppm\n";
+                 "\t--max-steps N (default 6000)  --precision fp32|bf16|fp16|fp32x3  --scene v1|tanh  --ppm\n";
 }
 
 static void parseCmdOptions(int argc, char **argv) {
@@ -76,7 +76,9 @@ static void parseCmdOptions(int argc, char **argv) {
     if (getCmdOption(b, e, "--scene")) NR_SCENE_MODE = std::string(getCmdOption(b, e, "--scene")) == "tanh" ? NR_SCENE_TANH : NR_SCENE_V1;
     if (getCmdOption(b, e, "--precision")) {
         std::string p = getCmdOption(b, e, "--precision");
-        NR_PRECISION_MODE = p == "bf16" ? NR_PRECISION_BF16 : (p == "fp16" ? NR_PRECISION_FP16 : NR_PRECISION_FP32);
+        NR_PRECISION_MODE = p == "bf16" ? NR_PRECISION_BF16
+                            : p == "fp16" ? NR_PRECISION_FP16
+                            : p == "fp32x3" ? NR_PRECISION_FP32X3 : NR_PRECISION_FP32;
     }
 }
 
