@@ -365,7 +365,26 @@ __device__ uint32_t shade_color(const RenderArgs &A, const float *nm, F3 n, F3 d
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// v of lane 4 * (l / 4) + Q of this lane's quad (DPP quad_perm: a VALU operand modifier, no LDS
+// round trip and no per-lane address register)
+template <int Q>
+__device__ __forceinline__ float quad_bcast(float v) {
+    constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xf, 0xf, false));
+}
+__device__ __forceinline__ F3 quad_bcast3_1(const F3 &v) { return mk3(quad_bcast<1>(v.x), quad_bcast<1>(v.y), quad_bcast<1>(v.z)); }
+__device__ __forceinline__ F3 quad_bcast3_2(const F3 &v) { return mk3(quad_bcast<2>(v.x), quad_bcast<2>(v.y), quad_bcast<2>(v.z)); }
+__device__ __forceinline__ F3 quad_bcast3_3(const F3 &v) { return mk3(quad_bcast<3>(v.x), quad_bcast<3>(v.y), quad_bcast<3>(v.z)); }
+
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// popcount(m & lanemask_lt()): the set lanes of m below this one, by v_mbcnt_lo / v_mbcnt_hi.
+// (Formed from lanemask_lt(), the per-lane 64-bit mask is a loop invariant the compiler hoists
+// out of the tracer's loop and keeps in two VGPRs for the kernel's life: the batched fp32
+// k_trace spilled it to scratch.)
+__device__ __forceinline__ uint32_t rank_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 // Position of the d-th (0-based) set bit of m (m must have more than d bits set).
 __device__ __forceinline__ int select_bit(uint64_t m, int d) {
@@ -398,8 +417,7 @@ __device__ __forceinline__ uint32_t wave_append(bool pred, uint32_t *counter) {
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(counter, cnt);
     base = __shfl(base, leader);
-    uint64_t below = m & ((1ull << lane) - 1ull);
-    return base + (uint32_t)__popcll(below);
+    return base + rank_below(m);
 }
 
 // Block-aggregated append to two queues: one atomic per queue per block.  Same-address
@@ -431,10 +449,9 @@ __device__ __forceinline__ Slots block_append2(bool pa, uint32_t *ca, bool pb, u
         s_tot[q] = tot;
     }
     __syncthreads();
-    const uint64_t below = (1ull << lane) - 1ull;
     Slots r;
-    r.a = s_app[0][16] + s_app[0][wv] + (uint32_t)__popcll(ma & below);
-    r.b = s_app[1][16] + s_app[1][wv] + (uint32_t)__popcll(mb & below);
+    r.a = s_app[0][16] + s_app[0][wv] + rank_below(ma);
+    r.b = s_app[1][16] + s_app[1][wv] + rank_below(mb);
     r.na = s_tot[0];
     r.nb = s_tot[1];
     __syncthreads();  // the arrays are reused by the next call

@@ -382,12 +382,9 @@ __device__ __forceinline__ void shade_rays(const RenderArgs &A, const float *nm,
     F3 tp = mk3(c_tet[3 * q], c_tet[3 * q + 1], c_tet[3 * q + 2]);
     F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
     F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff));
-    const int l0 = lane & ~3;
-    float c1x = __shfl(cq.x, l0 + 1), c1y = __shfl(cq.y, l0 + 1), c1z = __shfl(cq.z, l0 + 1);
-    float c2x = __shfl(cq.x, l0 + 2), c2y = __shfl(cq.y, l0 + 2), c2z = __shfl(cq.z, l0 + 2);
-    float c3x = __shfl(cq.x, l0 + 3), c3y = __shfl(cq.y, l0 + 3), c3z = __shfl(cq.z, l0 + 3);
+    const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
     if (live && q == 0) {
-        F3 acc = add3(add3(add3(cq, mk3(c1x, c1y, c1z)), mk3(c2x, c2y, c2z)), mk3(c3x, c3y, c3z));
+        F3 acc = add3(add3(add3(cq, c1), c2), c3);
         F3 nrm = normalize3(acc);
         out[pix] = shade_color(A, nm, nrm, mk3(sd.x, sd.y, sd.z));
     }

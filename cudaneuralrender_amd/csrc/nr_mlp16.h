@@ -19,12 +19,37 @@ namespace nr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// z_t lives in lane (j, 3) = 48 + j of tile t; point p = 16t + j gets it back in lane p.
+// Cross-lane moves by v_permlane{16,32}_swap (VALU, no LDS round trip, no per-lane address
+// register for the compiler to hoist out of the tracer's loop), on lane groups g = lane >> 4:
+//   permlane16_swap(a, b) = {[a0 b0 a2 b2], [a1 b1 a3 b3]},  permlane32_swap(a, b) = {[a0 a1 b0 b1], [a2 a3 b2 b3]}
+// (element k of a list = the 16 lanes of group k).
+__device__ __forceinline__ uint32_t pl16(uint32_t a, uint32_t b, int half) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    return half ? r[1] : r[0];
+}
+__device__ __forceinline__ uint32_t pl32(uint32_t a, uint32_t b, int half) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    return half ? r[1] : r[0];
+}
+
+// NT <= 2 tiles (the 3-4 tile form transposes instead): z_t lives in lane (j, 3) = 48 + j of tile t; point p = 16t + j gets it back
+// in lane p: [z0 g1, z1 g1, z0 g3, z1 g3], then the upper half's groups to the lower half.
+template <int NT>
 __device__ __forceinline__ float tile_outputs(const float zt[4]) {
-    const int lane = lane_id(), j = lane & 15, t = lane >> 4;
-    float r0 = __shfl(zt[0], 48 + j), r1 = __shfl(zt[1], 48 + j);
-    float r2 = __shfl(zt[2], 48 + j), r3 = __shfl(zt[3], 48 + j);
-    return t == 0 ? r0 : (t == 1 ? r1 : (t == 2 ? r2 : r3));
+    const uint32_t r = pl16(__float_as_uint(zt[0]), __float_as_uint(zt[NT > 1 ? 1 : 0]), 1);
+    return __uint_as_float(pl32(r, r, 1));
+}
+
+// The value group q - 1 holds, delivered to group q (q = 1, 2, 3; other groups: unspecified).
+__device__ __forceinline__ float from_prev_group(float v, int q) {
+    const uint32_t u = __float_as_uint(v);
+    if (q == 1) return __uint_as_float(pl16(u, u, 0));     // [v0 v0 v2 v2]
+    if (q == 2) {
+        const uint32_t t = pl16(u, u, 1);                  // [v1 v1 v3 v3]
+        return __uint_as_float(pl32(t, t, 0));             // [v1 v1 v1 v1]
+    }
+    const uint32_t t = pl32(u, u, 1);                      // [v2 v3 v2 v3]
+    return __uint_as_float(pl16(t, t, 0));                 // [v2 v2 v2 v2]
 }
 
 // FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
@@ -159,14 +184,14 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
         for (int k = 0; k < 8; ++k) acc = __builtin_fmaf(w8[k], a[t][k], acc);
 #pragma unroll
         for (int q = 1; q < 4; ++q) {
-            float nacc = __shfl(acc, (lane + 48) & 63);  // from lane - 16 (group g - 1)
+            float nacc = from_prev_group(acc, q);  // group g - 1's partial chain
 #pragma unroll
             for (int k = 0; k < 8; ++k) nacc = __builtin_fmaf(w8[k], a[t][k], nacc);
             acc = (g == q) ? nacc : acc;
         }
         zt[t] = acc + bf;
     }
-    return tile_outputs(zt);
+    return tile_outputs<NT>(zt);
 }
 
 // wave-uniform: every lane's inputs are within F32_INPUT_BOUND (NaN is not)

@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                 }
                 }
                 if (got) {
-                    const uint32_t rank = (uint32_t)__popcll(freem & lanemask_lt());
+                    const uint32_t rank = rank_below(freem);
                     bool hit = false;
                     if (it < 0 && rank < got) {
                         uint32_t q = base + rank;
@@ -363,10 +363,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
-            const int l0 = lane & ~3;
-            const F3 c1 = mk3(__shfl(cq.x, l0 + 1), __shfl(cq.y, l0 + 1), __shfl(cq.z, l0 + 1));
-            const F3 c2 = mk3(__shfl(cq.x, l0 + 2), __shfl(cq.y, l0 + 2), __shfl(cq.z, l0 + 2));
-            const F3 c3 = mk3(__shfl(cq.x, l0 + 3), __shfl(cq.y, l0 + 3), __shfl(cq.z, l0 + 3));
+            const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
             if (k < nb && q4 == 0 && !T.itmap) {
                 const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
                 const uint32_t pxl = __float_as_uint(sp.w);
@@ -457,7 +454,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         }
         const uint64_t cm = __ballot(conv);
         if (conv) {
-            const int slot = nstash + (int)__popcll(cm & lanemask_lt());
+            const int slot = nstash + (int)rank_below(cm);
             stash[wid][slot] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
             if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)rf;
         }

@@ -169,6 +169,42 @@ def test_device_code_has_no_packed_fp32(tmp_path):
     assert_no_packed_fp32(_lib.LIB_PATH, tmp_path)
 
 
+def kernel_resources(lib_path, tmp_path):
+    """{kernel symbol: {vgpr_count, private_segment_fixed_size, vgpr_spill_count, ...}} from the
+    code-object metadata of lib_path's gfx950 objects"""
+    import shutil
+    import subprocess
+    readelf, objdump = "/opt/rocm/lib/llvm/bin/llvm-readelf", "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not (os.path.exists(readelf) and os.path.exists(objdump)):
+        pytest.skip("llvm-readelf / llvm-objdump not available")
+    so = tmp_path / "libnr.so"
+    shutil.copy(lib_path, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    out = {}
+    for p in sorted(p for p in tmp_path.iterdir() if "amdgcn" in p.name and "gfx950" in p.name):
+        notes = subprocess.run([readelf, "--notes", str(p)], check=True, capture_output=True, text=True).stdout
+        for blk in notes.split(".name:")[1:]:
+            name = blk.split("\n")[0].strip()
+            out[name] = {k: int(v) for k, v in re.findall(r"\.(\w+):\s+(\d+)\s*$", blk, re.M)}
+    return out
+
+
+def test_batched_fp32_tracer_has_no_scratch(tmp_path):
+    """the bench's kernel -- the batched fp32 k_trace, built for 4 workgroups per
+    CU (<= 128 VGPRs) -- keeps every value in registers: no spill, no scratch.  (Its spills were
+    per-lane loop invariants the compiler hoisted: the lanemask of popcount(m & lanemask_lt()) and
+    the ds_bpermute addresses of the quad and lane-group shuffles; mbcnt, DPP quad_perm and
+    v_permlane swaps need none.)  The stand-alone MLP's fp32 and bf16 instances stay spill-free."""
+    res = kernel_resources(_lib.LIB_PATH, tmp_path)
+    want = {"_ZN2nr7k_traceILi0ELb0ELb0ELb1EEEvNS_10RenderArgsENS_7MlpArgsENS_9TraceArgsE": 128,
+            "_ZN2nr7k_mlp16ILi0ELi3EEEvNS_7MlpArgsEPKfPfi": 512,
+            "_ZN2nr7k_mlp16ILi1ELi3EEEvNS_7MlpArgsEPKfPfi": 512}
+    for name, cap in want.items():
+        r = res[name]
+        assert r["private_segment_fixed_size"] == 0 and r["vgpr_spill_count"] == 0, (name, r)
+        assert r["vgpr_count"] <= cap, (name, r)
+
+
 def test_batch_frames_per_launch_fits_the_queue_counters():
     """nr_render_batch caps the frames of one launch so that the busiest pixel-queue shard's
     positions (plus the waves' over-reservation) stay below 2^32 (16384^2 x 16
