@@ -1202,8 +1202,7 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 8;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
-            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16,
-                                          ((c->debug >> 7) & 1) | (((c->debug >> 11) & 1) << 1), s));
+            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
         else
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
     } else {

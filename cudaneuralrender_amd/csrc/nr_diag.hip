@@ -10,8 +10,8 @@ extern __shared__ __attribute__((aligned(16))) unsigned char nr_smem_diag[];
 // Latency of the fp32 MLP on NT tiles for one wave alone on its SIMD (nr_set_debug
 // bit 6): `reps` back-to-back evaluations, each input depending on the previous output.
 // Y[0] = shader cycles per evaluation, Y[1..64] = the last outputs.  PART: see
-// mlp16_fp32_nt; PF: the single-frame tracer's one-layer-ahead operand reads (one or two tiles).
-template <int NT, int PART, bool PF>
+// mlp16_fp32_nt.
+template <int NT, int PART>
 __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
                                                     int reps) {
     float *s32 = reinterpret_cast<float *>(nr_smem_diag);
@@ -22,31 +22,25 @@ __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__re
     float x = X[3 * lane], y = X[3 * lane + 1], z = X[3 * lane + 2], v = 0.0f;
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    for (int r = 0; r < reps; ++r) v = mlp16_fp32_nt<NT, PART, false, PF>(s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
+    for (int r = 0; r < reps; ++r) v = mlp16_fp32_nt<NT, PART>(s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
     Y[1 + lane] = v;
 }
 
-template <int PART, bool PF>
+template <int PART>
 static void launch_lat(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st) {
     const int sm = M.pk_bytes;
-    if (nt <= 1) hipLaunchKernelGGL((k_mlp_latency<1, PART, PF>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 2) hipLaunchKernelGGL((k_mlp_latency<2, PART, PF>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 3) hipLaunchKernelGGL((k_mlp_latency<3, PART, false>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else hipLaunchKernelGGL((k_mlp_latency<4, PART, false>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    if (nt <= 1) hipLaunchKernelGGL((k_mlp_latency<1, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 2) hipLaunchKernelGGL((k_mlp_latency<2, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 3) hipLaunchKernelGGL((k_mlp_latency<3, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else hipLaunchKernelGGL((k_mlp_latency<4, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
 }
 
-// part bit 0: without the final layer; bit 1: the prefetching form
 hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, int part, hipStream_t st) {
-    if (part & 2) {
-        if (part & 1) launch_lat<1, true>(M, X, Y, reps, nt, st);
-        else launch_lat<0, true>(M, X, Y, reps, nt, st);
-    } else {
-        if (part & 1) launch_lat<1, false>(M, X, Y, reps, nt, st);
-        else launch_lat<0, false>(M, X, Y, reps, nt, st);
-    }
+    if (part) launch_lat<1>(M, X, Y, reps, nt, st);
+    else launch_lat<0>(M, X, Y, reps, nt, st);
     return hipGetLastError();
 }
 

@@ -59,11 +59,7 @@ __device__ __forceinline__ float from_prev_group(float v, int q) {
 // where every activation is at most 1/2: bit-equal to fmaxf(v, 0) (NaN and -0 aside, which
 // the chains of the next layer map to the same values).  Every VALU instruction costs f32
 // matrix time on gfx950 (profiles/r1_mfma_peak.txt), and this halves the activation VALU.
-// NR_F32_PREFETCH 0: the one- and two-tile forms read each layer's operands at its start (A/B)
-#ifndef NR_F32_PREFETCH
-#define NR_F32_PREFETCH 1
-#endif
-template <int NT, int PART = 0, bool CL = false, bool PF = false>
+template <int NT, int PART = 0, bool CL = false>
 __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
                                                float y, float z) {
     auto relu = [](float v) { return CL ? __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f) : fmaxf(v, 0.0f); };
@@ -107,22 +103,12 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
 #pragma unroll
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = relu(__builtin_fmaf(c[t][mt][r], s0, bias[4 * mt + r]));
     }
-    // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile.
-    // With one or two tiles (the tail of a frame, where a wave's iteration latency is the frame's
-    // critical path) each layer's A operands and biases are read one layer ahead, so their LDS
-    // latency hides under the previous layer's MFMA chain instead of opening every layer
-    // (PF: the single-frame tracer only, whose tail it shortens; the 24 registers would make
-    // the batched tracer, the wavefront kernels and the stand-alone MLP spill).
-    constexpr bool PFX = PF && NR_F32_PREFETCH && NT <= 2;
-    auto load_w = [&](int jl, float4 (&w)[4], float4 (&b)[2]) {
+    // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
+    for (int jl = 0; jl < nh; ++jl) {
         const float *L = s + PK_HID + jl * PK_HID_STRIDE;
+        float4 wq[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = reinterpret_cast<const float4 *>(L)[q * 64 + lane];
-        const float4 *bb = reinterpret_cast<const float4 *>(L + 1024 + g * 8);
-        b[0] = bb[0];
-        b[1] = bb[1];
-    };
-    auto layer = [&](const float4 (&wq)[4], const float4 (&bw)[2]) {
+        for (int q = 0; q < 4; ++q) wq[q] = reinterpret_cast<const float4 *>(L)[q * 64 + lane];
 #pragma unroll
         for (int st = 0; st < 8; ++st) {
 #pragma unroll
@@ -136,40 +122,15 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
                         w, a[t][st], st == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : c[t][mt], 0, 0, 0);
             }
         }
-        const float bias[8] = {bw[0].x, bw[0].y, bw[0].z, bw[0].w, bw[1].x, bw[1].y, bw[1].z, bw[1].w};
+        const float4 *bb = reinterpret_cast<const float4 *>(L + 1024 + g * 8);
+        const float4 blo = bb[0], bhi = bb[1];
+        const float bias[8] = {blo.x, blo.y, blo.z, blo.w, bhi.x, bhi.y, bhi.z, bhi.w};
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = relu(c[t][mt][r] + bias[4 * mt + r]);
-    };
-    // the final 32 -> 1 layer's weights (group g's 8 units) and bias, for the one- and two-tile forms
-    float w8[8], bf = 0.0f;
-    auto load_final = [&]() {
-        const float *wf = s + pk_final(nh) + g * 8;
-        bf = s[pk_final(nh) + 32];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) w8[k] = wf[k];
-    };
-    if constexpr (PFX) load_final();
-    float4 wA[4], bA[2];
-    if constexpr (PFX) {
-        // two operand sets in ping-pong (no register copies between layers)
-        float4 wB[4], bB[2];
-        if (nh > 0) load_w(0, wA, bA);
-        for (int jl = 0; jl < nh; jl += 2) {
-            if (jl + 1 < nh) load_w(jl + 1, wB, bB);
-            layer(wA, bA);
-            if (jl + 1 >= nh) break;
-            if (jl + 2 < nh) load_w(jl + 2, wA, bA);
-            layer(wB, bB);
-        }
-    } else {
-        for (int jl = 0; jl < nh; ++jl) {
-            load_w(jl, wA, bA);
-            layer(wA, bA);
-        }
     }
     if constexpr (PART != 0) return a[0][0] + a[NT - 1][7];
     if constexpr (NT >= 3) {
@@ -210,8 +171,11 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
     }
     // final 32 -> 1 on VALU: group g holds units 8g..8g+7; the fmaf chain runs through
     // groups 0 -> 1 -> 2 -> 3 with one cross-lane hand-off per group.
-    // (the weights were read before the hidden layers when PFX)
-    if constexpr (!PFX) load_final();
+    const float *wf = s + pk_final(nh) + g * 8;
+    const float bf = s[pk_final(nh) + 32];
+    float w8[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) w8[k] = wf[k];
     float zt[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -245,15 +209,14 @@ __device__ __forceinline__ bool inputs_in_bound_f32(float x, float y, float z, f
 // bound -- the clamped form on the active tiles; otherwise (never on the bundled networks'
 // rays) the add + max form on all four tiles, which keeps one extra copy of the MLP code
 // in the kernels instead of four
-template <bool PF = false>
 __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
                                             float z, uint32_t tmask, bool cl) {
     const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
     if (NR_F32_CLAMP && cl) {
         if (nt >= 4) return mlp16_fp32_nt<4, 0, true>(s, in0, nh, fr, x, y, z);
         if (nt == 3) return mlp16_fp32_nt<3, 0, true>(s, in0, nh, fr, x, y, z);
-        if (nt == 2) return mlp16_fp32_nt<2, 0, true, PF>(s, in0, nh, fr, x, y, z);
-        return mlp16_fp32_nt<1, 0, true, PF>(s, in0, nh, fr, x, y, z);
+        if (nt == 2) return mlp16_fp32_nt<2, 0, true>(s, in0, nh, fr, x, y, z);
+        return mlp16_fp32_nt<1, 0, true>(s, in0, nh, fr, x, y, z);
     }
     if (NR_F32_CLAMP) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
     if (nt >= 4) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
@@ -261,10 +224,9 @@ __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0
     if (nt == 2) return mlp16_fp32_nt<2>(s, in0, nh, fr, x, y, z);
     return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
 }
-template <bool PF = false>
 __device__ __forceinline__ float mlp16_fp32(const MlpArgs &M, const float *s, float fr, float x, float y, float z,
                                             uint32_t tmask) {
-    return mlp16_fp32<PF>(s, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
+    return mlp16_fp32(s, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
 }
 
 // bf16 / fp16: the whole MLP on 32-point tiles, v_mfma_f32_32x32x16_{bf16,f16} (nr_internal.h
@@ -861,15 +823,13 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
 
 // cl: see mlp16_lowp (ignored in fp32); fp32x3: the pack is valid (M.lp_clamp), the inputs are
 // checked here
-// PF: one-layer-ahead operand reads in the fp32 MLP's one- and two-tile forms (mlp16_fp32_nt)
-template <bool PF = false>
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
     if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP32X3)
         return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0 && inputs_in_bound_x3(x, y, z, fr));
-    return mlp16_fp32<PF>(M, s32, fr, x, y, z, tmask);
+    return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }
 
 // wave-uniform: every lane's inputs are within LP_INPUT_BOUND (NaN is not)

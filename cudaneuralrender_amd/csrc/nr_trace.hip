@@ -404,8 +404,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
         if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
-        const float sdf = mlp16<!BATCH && !PROBE && !STAMPS>(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask,
-                                                           M.lp_clamp != 0);
+        const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);

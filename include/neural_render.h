@@ -204,8 +204,7 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
  * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and
  * A/B of the two forms); fp32x3 by the fp32 MLP for every wave (its fallback, bit-exact fp32).  Bit 10 = nr_render_batch deals its pixel queue frame after
- * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected).  Bit 11
- * = the bit-6 probe with the single-frame tracer's one-layer-ahead operand reads (1-2 tiles). */
+ * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next

@@ -15,10 +15,9 @@ X = torch.from_numpy(np.random.default_rng(0).uniform(-1, 1, (64, 3)).astype(np.
 Y = torch.zeros(65, dtype=torch.float32, device="cuda")
 # (the no-final-layer variant is meaningful for 1-2 tiles only: with more, the tiles whose
 # outputs it drops are dead code)
-# debug bit 11: the single-frame tracer's form (operands read one layer ahead, 1-2 tiles)
-for part, name in [(0, "full"), (1, "no final layer"), (16, "full, prefetch"), (17, "no final, prefetch")]:
+for part, name in [(0, "full"), (1, "no final layer")]:
     r.set_debug(64 | (part << 7))
-    for nt in ((1, 2) if part & 16 else (1, 2, 3, 4)):
+    for nt in (1, 2, 3, 4):
         r.set_wave_rays(16 * nt)
         for _ in range(2):
             r.mlp_forward_device(X.data_ptr(), Y.data_ptr(), 2000)
