@@ -1199,7 +1199,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // workgroups per CU: 8 (queued beyond the resident ones, they keep every SIMD fed
         // to the end of the batch): 2^24 points fp32 0.796 -> 0.825 of peak, bf16 (102 VGPRs,
         // 5 waves per SIMD resident) 0.352 -> 0.410 against 4 (profiles/r2_mlp_microbench.txt)
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 8;
+        // 12 workgroups per CU by default: more than fit at once (3-5), so that workgroups start
+        // staggered as earlier ones retire -- a grid of exactly the resident workgroups runs the
+        // bf16 MLP 17 % slower (its waves stay in step: profiles/r3_mlp_bpc.txt)
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 12;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
