@@ -362,6 +362,13 @@ __device__ uint32_t shade_color(const RenderArgs &A, const float *nm, F3 n, F3 d
     return A.matcap[index];
 }
 
+// initMarcher's (x / (float)imageW) * 2 - 1 (:315-316); with a power-of-two divisor (rcp = 1/W, else 0)
+// the quotient is the product by the exact reciprocal, bit for bit
+__device__ __forceinline__ float pixel_uv(int x, int W, float rcp) {
+    const float q = rcp != 0.0f ? (float)x * rcp : (float)x / (float)W;
+    return q * 2.0f - 1.0f;
+}
+
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -29,10 +29,17 @@ struct RenderArgs {
     float inv_view[12];
     float normal[16];
     double inv_w, inv_band;  // 1/W, 1/band for udiv_r (set_recips)
+    // 1/W, 1/H where W (H) is a power of two, else 0: initMarcher's (float)x / (float)W is then
+    // (float)x * (1/W) exactly (a power-of-two divisor only shifts the exponent), which saves
+    // ray generation two correctly rounded divisions (set_recips; pixel_uv)
+    float rcp_w, rcp_h;
 };
+inline float pow2_rcp(int n) { return n > 0 && (n & (n - 1)) == 0 ? 1.0f / (float)n : 0.0f; }
 inline void set_recips(RenderArgs &A) {
     A.inv_w = 1.0 / (double)A.W;
     A.inv_band = 1.0 / (double)A.band;
+    A.rcp_w = pow2_rcp(A.W);
+    A.rcp_h = pow2_rcp(A.H);
 }
 
 // Ray queues: live rays {p.xyz, tfar} + {d.xyz, pixel}; converged rays {p.xyz, -} + {d.xyz, pixel}.

@@ -320,8 +320,8 @@ __device__ __forceinline__ bool gen_hit(const RenderArgs &A, const float *M, lon
     const int y = (bi * A.nshards + A.shard) * A.band + (lr - bi * A.band);
     F3 o = mk3(dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 0), dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 4),
                dot4(0.0f, 0.0f, 0.0f, 1.0f, M + 8));
-    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
-    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
+    float u = pixel_uv(x, A.W, A.rcp_w);
+    float v = pixel_uv(y, A.H, A.rcp_h);
     F3 d = normalize3(mk3(u, v, -2.0f));
     d = mk3(dot3(d, mk3(M[0], M[1], M[2])), dot3(d, mk3(M[4], M[5], M[6])), dot3(d, mk3(M[8], M[9], M[10])));
     // intersectSphere (:199-215), bounding sphere c = 0, r = 1.2

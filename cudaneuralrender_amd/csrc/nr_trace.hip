@@ -87,8 +87,8 @@ __device__ __forceinline__ int shard_row(const RenderArgs &A, const TraceArgs &T
 // The ray direction of pixel x of local row lr (initMarcher :293-358).
 __device__ __forceinline__ F3 ray_dir(const RenderArgs &A, const TraceArgs &T, const float *M, int x, int lr) {
     const int y = shard_row(A, T, lr);
-    float u = ((float)x / (float)A.W) * 2.0f - 1.0f;
-    float v = ((float)y / (float)A.H) * 2.0f - 1.0f;
+    float u = pixel_uv(x, A.W, A.rcp_w);
+    float v = pixel_uv(y, A.H, A.rcp_h);
     F3 dd = normalize3(mk3(u, v, -2.0f));
     return mk3(dot3(dd, mk3(M[0], M[1], M[2])), dot3(dd, mk3(M[4], M[5], M[6])), dot3(dd, mk3(M[8], M[9], M[10])));
 }
