@@ -839,9 +839,12 @@ __device__ __forceinline__ bool inputs_in_bound(float x, float y, float z, float
     return __ballot(!ok) == 0;
 }
 
+// the 16-lane tiles of lane mask m that hold a set lane -- on the 32-bit halves: as a 64-bit test,
+// m >> 48 != 0 became a compare against the constant 2^48, which the compiler kept in a VGPR pair
+// for the tracer's whole life (and spilled)
 __device__ __forceinline__ uint32_t tiles_of(uint64_t m) {
-    return ((m & 0xffffull) ? 1u : 0u) | (((m >> 16) & 0xffffull) ? 2u : 0u) | (((m >> 32) & 0xffffull) ? 4u : 0u) |
-           ((m >> 48) ? 8u : 0u);
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    return ((lo & 0xffffu) ? 1u : 0u) | ((lo >> 16) ? 2u : 0u) | ((hi & 0xffffu) ? 4u : 0u) | ((hi >> 16) ? 8u : 0u);
 }
 
 // LDS staging of the 16-wide packs (dynamic shared memory, block-wide 16-byte copies)

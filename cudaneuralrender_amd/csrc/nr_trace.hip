@@ -184,7 +184,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
     auto put = [&](int f, uint32_t i, uint32_t v) { out_of(f)[i] = v; };
     const int q4 = lane & 3;
-    const F3 tp = mk3(c_tet[3 * q4], c_tet[3 * q4 + 1], c_tet[3 * q4 + 2]);
     int nstash = 0;
     const int nq = 1 << T.nq_shift;  // pixel-queue shards
     int shard = blockIdx.x & (nq - 1), tries = 0;
@@ -359,6 +358,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             const float4 sp = stash[wid][e];
             const int sfr = BATCH ? (int)stash_f[wid][e] : 0;
+            // tetrahedron point q4 (c_tet, :38-43) formed here from an opaque copy of the lane
+            // index, so that the compiler does not hoist it out of the loop into three VGPRs
+            // held for the kernel's life: x = +1 for q = 0, 3; y = +1 for q = 2, 3; z = +1 for q = 1, 3
+            int qo = q4;
+            asm volatile("" : "+v"(qo));
+            const F3 tp = mk3((qo == 0 || qo == 3) ? 1.0f : -1.0f, qo >= 2 ? 1.0f : -1.0f, (qo & 1) ? 1.0f : -1.0f);
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
