@@ -61,6 +61,10 @@ namespace nr {
 #define NR_QUEUE_LOW 8
 #endif
 
+#ifndef NR_DENSE_GEN
+#define NR_DENSE_GEN 1
+#endif
+
 // Refill only once this many ray slots are free (or the wave is empty), so that the ray
 // generation and the queue bookkeeping are paid for several rays at a time: bf16 batch
 // 0.611 -> 0.571 ms/frame at 8 (4: 0.589, 16: 0.575), fp32 1.978 -> 1.964 at 4
@@ -155,6 +159,8 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
+    // rays generated in bulk through an LDS buffer (NR_DENSE_GEN): the reduced-precision tracers
+    constexpr bool DENSE = NR_DENSE_GEN && PREC != NR_PRECISION_FP32 && !PROBE;
     __shared__ FrameLds sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
         for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // 18 words per FrameLds
@@ -170,6 +176,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // so that 4 fp32 workgroups share a CU
     __shared__ float4 stash[4][STASH];
     __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
+    // DENSE: per wave a ring of 64 generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame): 8.25 KB
+    __shared__ float4 rbuf[DENSE ? 4 : 1][DENSE ? 64 : 1][2];
+    __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? 64 : 1];
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -190,6 +199,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     bool qempty = false;
     uint32_t pool_base = 0, pool_cnt = 0, pend_v = 0;  // NR_QUEUE_PREFETCH state
     bool pend = false;
+    uint32_t rb_n = 0, rb_head = 0;  // DENSE: rays in the wave's buffer, ring position of the first
     bool hold = false;  // age hold (TraceArgs::hold_age): no refill, packed tiles, raised priority
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
     float tfar = 0.0f;
@@ -214,144 +224,215 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         pool_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_base);
         pool_cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_cnt);
         pend = __builtin_amdgcn_readfirstlane((int)pend) != 0;
+        rb_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_n);
+        rb_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_head);
         // ---- refill free slots from the pixel queue
-        if (!qempty && !(hold && !T.hold_refill)) {
+        if ((!qempty || (DENSE && rb_n > 0)) && !(hold && !T.hold_refill)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
             const uint64_t freem = __ballot(it < 0) & T.lane_cap;
             const uint32_t nfree = (uint32_t)__popcll(freem);
-            if (nfree >= (uint32_t)RMIN || (nfree && nfree == (uint32_t)T.take)) {
-                uint32_t base = 0, got = 0;
+            // (a drained queue's buffered rays are dealt at once: they are the frame's last)
+            if (nfree >= (uint32_t)RMIN || (nfree && nfree == (uint32_t)T.take) || (DENSE && qempty && nfree)) {
                 auto shard_total = [&](int sh) -> long {
                     const long sh_chunks = sh < nchunks ? ((nchunks - 1 - sh) >> T.nq_shift) + 1 : 0;
                     return (PROBE ? sh_chunks : sh_chunks * 64) * (BATCH ? T.nframes : 1);
                 };
-                // Queue positions are broadcast with readfirstlane (the whole wave is active
-                // here), not __shfl, so that the compiler sees them as uniform and keeps the
-                // queue logic in scalar branches instead of lane-mask control flow.
-                if constexpr (QPF) {
-                // Positions come from a wave-private pool of reserved queue positions; the
-                // next reservation is requested (one atomic, not waited for) when the pool
-                // runs low and absorbed when it is empty, so its ~1 us return latency
-                // overlaps the MLP instead of stalling the refill.
-                if (pool_cnt == 0) {
-                    if (pend) {
-                        const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend_v);
-                        pend = false;
-                        const long tot = shard_total(shard);
-                        if ((long)b < tot) {
-                            pool_base = b;
-                            pool_cnt = (uint32_t)min((long)NR_QUEUE_CHUNK, tot - (long)b);
+                // Up to `want` positions of the queue -> [base, base + got).  Queue positions are
+                // broadcast with readfirstlane (the whole wave is active here), not __shfl, so
+                // that the compiler sees them as uniform and keeps the queue logic in scalar
+                // branches instead of lane-mask control flow.
+                auto reserve = [&](uint32_t want, uint32_t &base, uint32_t &got) {
+                    got = 0;
+                    if constexpr (QPF) {
+                        // Positions come from a wave-private pool of reserved queue positions;
+                        // the next reservation is requested (one atomic, not waited for) when the
+                        // pool runs low and absorbed when it is empty, so its ~1 us return
+                        // latency overlaps the MLP instead of stalling the refill.
+                        if (pool_cnt == 0) {
+                            if (pend) {
+                                const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend_v);
+                                pend = false;
+                                const long tot = shard_total(shard);
+                                if ((long)b < tot) {
+                                    pool_base = b;
+                                    pool_cnt = (uint32_t)min((long)NR_QUEUE_CHUNK, tot - (long)b);
+                                }
+                            }
+                            while (pool_cnt == 0) {  // nothing reserved: a blocking reservation
+                                const long tot = shard_total(shard);
+                                const uint32_t w = max(want, (uint32_t)NR_QUEUE_CHUNK);
+                                uint32_t b = 0;
+                                if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, w);
+                                b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);  // lane 0: the whole wave is active
+                                if ((long)b < tot) {
+                                    pool_base = b;
+                                    pool_cnt = (uint32_t)min((long)w, tot - (long)b);
+                                    break;
+                                }
+                                shard = (shard + 1) & (nq - 1);
+                                if (++tries >= nq) {
+                                    qempty = true;
+                                    if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
+                                    break;
+                                }
+                            }
+                        }
+                        if (pool_cnt) {
+                            base = pool_base;
+                            got = min(want, pool_cnt);
+                            pool_base += got;
+                            pool_cnt -= got;
+                        }
+                        if (!qempty && !pend && pool_cnt < NR_QUEUE_LOW) {
+                            if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)NR_QUEUE_CHUNK);
+                            pend = true;
+                        }
+                    } else {
+                        while (true) {
+                            const long total = shard_total(shard);
+                            uint32_t b = 0;
+                            if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, want);
+                            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+                            if ((long)base < total) {
+                                got = (uint32_t)min((long)want, total - (long)base);
+                                break;
+                            }
+                            shard = (shard + 1) & (nq - 1);
+                            if (++tries >= nq) {
+                                qempty = true;
+                                if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
+                                break;
+                            }
                         }
                     }
-                    while (pool_cnt == 0) {  // nothing reserved: a blocking reservation
-                        const long tot = shard_total(shard);
-                        const uint32_t want = max(nfree, (uint32_t)NR_QUEUE_CHUNK);
-                        uint32_t b = 0;
-                        if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, want);
-                        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);  // lane 0: the whole wave is active
-                        if ((long)b < tot) {
-                            pool_base = b;
-                            pool_cnt = (uint32_t)min((long)want, tot - (long)b);
-                            break;
-                        }
-                        shard = (shard + 1) & (nq - 1);
-                        if (++tries >= nq) {
-                            qempty = true;
-                            if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
-                            break;
+                };
+                // The frame f and pixel (px, py) of queue position q; false outside the image.
+                auto pixel_of = [&](uint32_t q, int &f, int &px, int &py) -> bool {
+                    f = 0;
+                    if constexpr (BATCH) {
+                        if (T.interleave) {  // 64-position chunk c goes to frame c % n
+                            const uint32_t c = q >> 6, cq = udiv_r(c, (uint32_t)T.nframes, T.inv_nframes);
+                            f = (int)(c - cq * (uint32_t)T.nframes);
+                            q = (cq << 6) | (q & 63u);
+                        } else {  // frame-major: frame f owns [f * per, (f + 1) * per)
+                            const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
+                            f = (int)udiv_r(q, per, 1.0 / (double)per);
+                            q -= (uint32_t)f * per;
                         }
                     }
-                }
-                if (pool_cnt) {
-                    base = pool_base;
-                    got = min(nfree, pool_cnt);
-                    pool_base += got;
-                    pool_cnt -= got;
-                }
-                if (!qempty && !pend && pool_cnt < NR_QUEUE_LOW) {
-                    if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)NR_QUEUE_CHUNK);
-                    pend = true;
-                }
+                    uint32_t bq = q >> 6, pq = q & 63;
+                    if (PROBE) {
+                        bq = q;
+                        pq = 4 * 8 + 4;  // the block's centre pixel
+                    } else if (T.spread_shift) {
+                        const int sh = T.spread_shift;
+                        const uint32_t G = 1u << sh;
+                        const uint32_t sh_chunks = (uint32_t)(((nchunks - 1 - shard) >> T.nq_shift) + 1);
+                        const uint32_t g = q >> (6 + sh), r = q & ((64u << sh) - 1u);
+                        const uint32_t nbg = min(G, sh_chunks - g * G);
+                        pq = nbg == G ? r >> sh : r / nbg;  // a short group only at the end
+                        bq = g * G + (r - pq * nbg);
+                    }
+                    const long pos = ((long)bq << T.nq_shift) + shard;
+                    const int blk = T.order ? (int)T.order[pos] : (int)pos;
+                    const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
+                    px = bx * 8 + (pq & 7);
+                    py = by * 8 + (pq >> 3);
+                    if (PROBE) {
+                        px = min(px, A.W - 1);
+                        py = min(py, A.rows - 1);
+                    }
+                    return px < A.W && py < A.rows;
+                };
+                if constexpr (DENSE) {
+                    // Ray generation in bulk: when the buffer holds fewer rays than there are free
+                    // slots, every lane of the wave generates the ray of one reserved position
+                    // (up to 64 - rb_n of them) -- instead of only the few lanes a refill frees,
+                    // with the rest of the wave idle through initMarcher's divisions and square
+                    // roots -- and the hits are appended to the wave's LDS ray buffer (a ring
+                    // of 64); background pixels are written at once.  The free slots then take
+                    // rays from the buffer in order.
+                    // (a wave capped at T.take lanes buffers at most that many rays, so that a small
+                    // launch's rays stay spread over the waves)
+                    if (rb_n < nfree && !qempty) {
+                        uint32_t base = 0, got = 0;
+                        reserve((uint32_t)T.take - rb_n, base, got);
+                        bool hit = false, keep = false;
+                        F3 gp = mk3(0.0f, 0.0f, 0.0f), gd = mk3(0.0f, 0.0f, 0.0f);
+                        float gt = 0.0f;
+                        uint32_t glp = 0;
+                        int gf = 0;
+                        if ((uint32_t)lane < got) {
+                            int px, py;
+                            if (pixel_of(base + (uint32_t)lane, gf, px, py)) {
+                                glp = (uint32_t)((long)py * A.W + px);
+                                hit = gen_ray(A, T, BATCH ? sf[gf].inv_view : A.inv_view, px, py, gp, gd, gt);
+                                keep = hit && A.max_steps > 0;
+                                if (!keep) put(gf, glp, 0u);  // background (:335-339) or no iterations at all
+                            }
+                        }
+                        nhit += (uint64_t)__popcll(__ballot(hit));
+                        const uint64_t km = __ballot(keep);
+                        if (keep) {
+                            const uint32_t slot = (rb_head + rb_n + rank_below(km)) & 63u;
+                            rbuf[wid][slot][0] = make_float4(gp.x, gp.y, gp.z, gt);
+                            rbuf[wid][slot][1] = make_float4(gd.x, gd.y, gd.z, __uint_as_float(glp));
+                            if constexpr (BATCH) rbuf_f[wid][slot] = (uint8_t)gf;
+                        }
+                        rb_n += (uint32_t)__popcll(km);
+                    }
+                    const uint32_t take = min(nfree, rb_n);
+                    if (take) {
+                        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                        const uint32_t rank = rank_below(freem);
+                        if (it < 0 && rank < take) {
+                            const uint32_t slot = (rb_head + rank) & 63u;
+                            const float4 ra = rbuf[wid][slot][0], rd = rbuf[wid][slot][1];
+                            p = mk3(ra.x, ra.y, ra.z);
+                            tfar = ra.w;
+                            d = mk3(rd.x, rd.y, rd.z);
+                            pix = __float_as_uint(rd.w);
+                            if constexpr (BATCH) rf = (int)rbuf_f[wid][slot];
+                            it = 0;
+                        }
+                        rb_head = (rb_head + take) & 63u;
+                        rb_n -= take;
+                    }
                 } else {
-                while (true) {
-                    const long total = shard_total(shard);
-                    uint32_t b = 0;
-                    if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, nfree);
-                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-                    if ((long)base < total) {
-                        got = (uint32_t)min((long)nfree, total - (long)base);
-                        break;
-                    }
-                    shard = (shard + 1) & (nq - 1);
-                    if (++tries >= nq) {
-                        qempty = true;
-                        if (STAMPS) t_empty = __builtin_amdgcn_s_memrealtime();
-                        break;
-                    }
-                }
-                }
-                if (got) {
-                    const uint32_t rank = rank_below(freem);
-                    bool hit = false;
-                    if (it < 0 && rank < got) {
-                        uint32_t q = base + rank;
-                        int f = 0;
-                        if constexpr (BATCH) {
-                            if (T.interleave) {  // 64-position chunk c goes to frame c % n
-                                const uint32_t c = q >> 6, cq = udiv_r(c, (uint32_t)T.nframes, T.inv_nframes);
-                                f = (int)(c - cq * (uint32_t)T.nframes);
-                                q = (cq << 6) | (q & 63u);
-                            } else {  // frame-major: frame f owns [f * per, (f + 1) * per)
-                                const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
-                                f = (int)udiv_r(q, per, 1.0 / (double)per);
-                                q -= (uint32_t)f * per;
+                    uint32_t base = 0, got = 0;
+                    reserve(nfree, base, got);
+                    if (got) {
+                        const uint32_t rank = rank_below(freem);
+                        bool hit = false;
+                        if (it < 0 && rank < got) {
+                            int f, px, py;
+                            if (pixel_of(base + rank, f, px, py)) {
+                                const long lp = (long)py * A.W + px;
+                                hit = gen_ray(A, T, BATCH ? sf[f].inv_view : A.inv_view, px, py, p, d, tfar);
+                                if (hit && A.max_steps > 0) {
+                                    it = 0;
+                                    pix = (uint32_t)lp;
+                                    rf = f;
+                                } else if (!PROBE) {
+                                    put(f, lp, 0u);  // background (:335-339) or no iterations at all
+                                }
                             }
                         }
-                        uint32_t bq = q >> 6, pq = q & 63;
-                        if (PROBE) {
-                            bq = q;
-                            pq = 4 * 8 + 4;  // the block's centre pixel
-                        } else if (T.spread_shift) {
-                            const int sh = T.spread_shift;
-                            const uint32_t G = 1u << sh;
-                            const uint32_t sh_chunks = (uint32_t)(((nchunks - 1 - shard) >> T.nq_shift) + 1);
-                            const uint32_t g = q >> (6 + sh), r = q & ((64u << sh) - 1u);
-                            const uint32_t nbg = min(G, sh_chunks - g * G);
-                            pq = nbg == G ? r >> sh : r / nbg;  // a short group only at the end
-                            bq = g * G + (r - pq * nbg);
-                        }
-                        const long pos = ((long)bq << T.nq_shift) + shard;
-                        const int blk = T.order ? (int)T.order[pos] : (int)pos;
-                        const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
-                        int px = bx * 8 + (pq & 7), py = by * 8 + (pq >> 3);
-                        if (PROBE) {
-                            px = min(px, A.W - 1);
-                            py = min(py, A.rows - 1);
-                        }
-                        const long lp = (long)py * A.W + px;
-                        if (px < A.W && py < A.rows) {
-                            hit = gen_ray(A, T, BATCH ? sf[f].inv_view : A.inv_view, px, py, p, d, tfar);
-                            if (hit && A.max_steps > 0) {
-                                it = 0;
-                                pix = (uint32_t)lp;
-                                rf = f;
-                            } else if (!PROBE) {
-                                put(f, lp, 0u);  // background (:335-339) or no iterations at all
-                            }
-                        }
+                        nhit += (uint64_t)__popcll(__ballot(hit));
                     }
-                    nhit += (uint64_t)__popcll(__ballot(hit));
                 }
             }
         }
+        // the queue drained and no ray left to deal: the tail of the launch
+        const bool drained = qempty && (!DENSE || rb_n == 0);
         // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass.
         // Once the queue is drained a partial pass waits until the wave's last ray has
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
         // its size, and the marching rays must not wait for it.
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
         uint64_t lm = __ballot(it >= 0);
-        while (nstash >= 16 || (qempty && nstash > 0 && !lm)) {
+        while (nstash >= 16 || (drained && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
@@ -386,12 +467,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         }
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; tph = t; }
         if (!lm) {
-            if (qempty && nstash == 0) break;
+            if (drained && nstash == 0) break;
             continue;
         }
         uint32_t tmask = tiles_of(lm);
         // ---- tail / age hold: pack the live rays into the lowest tiles
-        if (qempty || (hold && !T.hold_refill)) {
+        if (drained || (hold && !T.hold_refill)) {
             const int nl = (int)__popcll(lm);
             const int need = (nl + 15) >> 4;
             if (__popc(tmask) > need) {
@@ -418,7 +499,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         }
         nsteps += (uint64_t)__popcll(lm);
         ++wit;
-        wit_tail += qempty ? 1u : 0u;
+        wit_tail += drained ? 1u : 0u;
         bool conv = false;
         if (it >= 0) {
             const float ts = scene_sdf(p, sdf, A.scene, zoff_of(rf));
