@@ -64,6 +64,10 @@ namespace nr {
 #ifndef NR_DENSE_GEN
 #define NR_DENSE_GEN 1
 #endif
+// (fp32: A/B only -- its ring would cost the batched instance its fourth workgroup per CU)
+#ifndef NR_DENSE_GEN_FP32
+#define NR_DENSE_GEN_FP32 0
+#endif
 
 // Refill only once this many ray slots are free (or the wave is empty), so that the ray
 // generation and the queue bookkeeping are paid for several rays at a time: bf16 batch
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     // rays generated in bulk through an LDS buffer (NR_DENSE_GEN): the reduced-precision tracers
-    constexpr bool DENSE = NR_DENSE_GEN && PREC != NR_PRECISION_FP32 && !PROBE;
+    constexpr bool DENSE = NR_DENSE_GEN && (PREC != NR_PRECISION_FP32 || NR_DENSE_GEN_FP32) && !PROBE;
     __shared__ FrameLds sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
         for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // 18 words per FrameLds
