@@ -88,6 +88,8 @@ def parse():
                     help="skip config.fp32x3 (the same frames timed in NR_PRECISION_FP32X3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-frame", action="store_true")
+    ap.add_argument("--no-spin", action="store_true",
+                    help="skip config.spin (the reference's --spin sequence, one launch per frame)")
     ap.add_argument("--no-random-poses", action="store_true",
                     help="skip config.random_poses (profiling passes that average the default-pose launches)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -303,6 +305,45 @@ def main():
     if not a.no_single_frame:
         dt_single, _, rs_single, _, _ = timed(run_single, False)
 
+    # The reference's own single-frame use, main.cpp --spin (doABarrelRoll, :470-477): frame i at
+    # viewRotation.y = i degrees with frameNumber = i, one launch per frame, timed with and without
+    # nr_set_temporal_order (each launch deals its 8x8 blocks longest-first by the PREVIOUS frame's
+    # block costs -- a different pose -- so the order is not taken from the frames it times).
+    # Single GPU only; the last timed frame is checked against a plain nr_render of its pose.
+    spin = None
+    if world == 1 and not a.no_spin and not a.no_single_frame:
+        spin_i = [0]
+
+        def run_spin(n):
+            with torch.cuda.stream(stream):
+                for _ in range(n):
+                    i = spin_i[0]
+                    spin_i[0] += 1
+                    ivs, nms = nr.camera(0.0, float(i % 360), 2.0)
+                    r.set_view(ivs, nms, i)
+                    st = r.render_shard_device(shards[i % nbuf].data_ptr(), size, size, BAND, 1, 0, a.max_steps,
+                                               with_stats=True)
+                    counted["ray_steps"] += st["ray_steps"]
+                    counted["shade_evals"] += st["shade_evals"]
+
+        spin = {"sequence": "frame i at viewRotation.y = i deg, frameNumber = i (main.cpp --spin, :470-477), "
+                            "one nr_render_shard launch per frame"}
+        for key, order in (("plain", 0), ("temporal_order", 1)):
+            spin_i[0] = 0
+            r.set_temporal_order(order)
+            dts, _, rss, _, _ = timed(run_spin, False)
+            spin[key] = {"value": round(rss / dts / 1e6, 3), "ms_per_step": round(dts / a.steps * 1e3, 4),
+                         "fps": round(a.steps / dts, 3)}
+        r.set_temporal_order(0)
+        last = spin_i[0] - 1
+        ivs, nms = nr.camera(0.0, float(last % 360), 2.0)
+        r.set_view(ivs, nms, last)
+        img = r.render(size, size, a.max_steps, with_stats=False)
+        ref_last = torch.from_numpy(img.view(np.int32).reshape(-1)).to("cuda")
+        spin["parity_last_frame_vs_plain_render"] = bool(torch.equal(shards[last % nbuf][: size * size], ref_last))
+        r.set_view(iv, nm, 0)
+        torch.cuda.synchronize()
+
     # the same timing over 8 random poses, frames cycling through them
     dt_pose = None
     if not a.no_random_poses:
@@ -413,6 +454,7 @@ def main():
                 "fps": round(a.steps / dt_single, 3),
                 "schedule": "one nr_render_shard launch per frame",
             },
+            "spin": spin,
             "random_poses": None if dt_pose is None else {
                 "value": round(rs_pose / dt_pose / 1e6, 3),
                 "ms_per_step": round(dt_pose / a.steps * 1e3, 4),
