@@ -328,7 +328,7 @@ def main():
 
         spin = {"sequence": "frame i at viewRotation.y = i deg, frameNumber = i (main.cpp --spin, :470-477), "
                             "one nr_render_shard launch per frame"}
-        for key, order in (("plain", 0), ("temporal_order", 1)):
+        for key, order in (("plain", 0), ("temporal_order", 1), ("temporal_order_dilated", 2)):
             spin_i[0] = 0
             r.set_temporal_order(order)
             dts, _, rss, _, _ = timed(run_spin, False)

@@ -944,7 +944,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         HIPCHK(c, launch_trace(A, mlp_for_frames(c, frames, nframes, 0), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         if (c->temporal) {  // the order for the next launch of this shape
-            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, 0, s));
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, c->temporal > 1, s));
             c->order_cur ^= 1;
             c->order_valid = 1;
         }
@@ -1111,7 +1111,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         HIPCHK(c, launch_trace(A, mlp_for_frames(c, nullptr, 0, A.frame), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
         if (c->temporal) {  // order for the next frame of the same configuration
-            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, 0, s));
+            HIPCHK(c, launch_order(c->d_bcost, c->d_order[c->order_cur ^ 1], T.nblocks, T.bw, c->temporal > 1, s));
             c->order_cur ^= 1;
             c->order_valid = 1;
         }
@@ -1292,7 +1292,7 @@ int nr_set_schedule(nr_ctx *c, int schedule) {
 
 int nr_set_temporal_order(nr_ctx *c, int on) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
-    c->temporal = on != 0;
+    c->temporal = on < 0 ? 0 : (on > 2 ? 2 : on);
     c->order_valid = 0;
     return NR_OK;
 }

@@ -209,7 +209,8 @@ int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next
  * launch of the same size/shard dispenses blocks longest-first (pixels are unaffected --
- * only the order work is handed out changes). */
+ * only the order work is handed out changes).  on = 2: each block's cost is the max over its
+ * 3x3 neighbourhood (for a moving camera, whose silhouettes shift between frames). */
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
