@@ -250,6 +250,30 @@ def test_temporal_order_same_pixels(rend, nets, chrome, W, H):
     assert sa["ray_steps"] == sb["ray_steps"] == sc["ray_steps"]
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_temporal_order_spin_same_pixels(rend, nets, chrome, mode):
+    """The reference's --spin sequence (frame i at ry = i deg, frameNumber i; main.cpp:470-477)
+    with the previous frame's block order, plain (1) and dilated over 3x3 blocks (2): every frame
+    equals its plain render."""
+    dims, K, B = nets["plane_1"]
+    rend.load_mlp(dims, K, B).set_precision("fp32")
+    rend.set_static(1, 3).set_scene("v1").set_matcap(chrome)
+    plain = []
+    for i in range(3):
+        iv, nm = nr.camera(0, float(i), 2)
+        rend.set_view(iv, nm, i)
+        plain.append(rend.render(256, 192, 128))
+    try:
+        rend.set_temporal_order(mode)
+        for i in range(3):
+            iv, nm = nr.camera(0, float(i), 2)
+            rend.set_view(iv, nm, i)
+            img, st = rend.render(256, 192, 128)
+            assert np.array_equal(img, plain[i][0]) and st["ray_steps"] == plain[i][1]["ray_steps"], (mode, i)
+    finally:
+        rend.set_temporal_order(False)
+
+
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
 def test_temporal_order_batch_same_pixels(rend, nets, chrome, prec):
     """nr_render_batch with the temporal order: the first batch records its block costs, the
