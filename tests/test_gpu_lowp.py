@@ -121,3 +121,33 @@ def test_mlp_128_point_form_equals_64_point_form(rend, nets, prec, debug):
     finally:
         rend.set_debug(0)
         rend.set_precision("fp32")
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_lowp_ragged_frames_schedules_agree(rend, nets, chrome, prec):
+    """The bf16/fp16 persistent tracers generate rays in bulk into a per-wave LDS ring
+    (nr_trace.hip, DENSE): tiny and ragged frames, 0/1/7 march steps, lane caps of 1-64 rays per
+    wave and batched launches all give the wavefront schedule's pixels and ray-steps (a separate
+    kernel path with the same per-ray arithmetic)."""
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1")
+    rend.set_matcap(chrome)
+    iv, nm = nr.camera(-10.0, 25.0, 2.0)
+    cams = [(*nr.camera(-10.0 + 7 * i, 25.0 + 40 * i, 2.0), i) for i in range(5)]
+    try:
+        for W, H, steps in [(1, 1, 128), (3, 5, 128), (65, 1, 128), (1, 67, 128), (130, 3, 128),
+                            (97, 61, 0), (97, 61, 1), (97, 61, 7), (200, 131, 128)]:
+            rend.set_view(iv, nm, 0).set_schedule("wavefront")
+            ref, sref = rend.render(W, H, steps)
+            bref, bsref = rend.render_batch(W, H, cams, steps)
+            rend.set_schedule("persistent")
+            for rays in (64, 16, 5, 1):
+                rend.set_wave_rays(rays).set_view(iv, nm, 0)
+                img, st = rend.render(W, H, steps)
+                assert np.array_equal(img, ref), (W, H, steps, rays)
+                assert st["ray_steps"] == sref["ray_steps"] and st["rays_shaded"] == sref["rays_shaded"], (W, H, steps, rays)
+                imgs, bst = rend.render_batch(W, H, cams, steps)
+                assert all(np.array_equal(x, y) for x, y in zip(imgs, bref)), (W, H, steps, rays)
+                assert bst["ray_steps"] == bsref["ray_steps"], (W, H, steps, rays)
+    finally:
+        rend.set_wave_rays(64).set_schedule("persistent").set_precision("fp32").set_view(*nr.camera(0, 0, 2), 0)
