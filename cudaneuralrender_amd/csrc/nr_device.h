@@ -236,14 +236,25 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // is beyond the running value + k in every lane: when that holds for the whole wave, the
     // sphere costs v_sqrt_f32 and the test instead of the correction, the sub and the union --
     // bit for bit the same result.  Spheres that some lane is near take the exact path.
+    //
+    // The test runs on the squared distance (round 3, later): sphere i is far when q[i] >= T2 =
+    // max(T, 0)^2 with T = (nsdf + 0.11f) + (|nsdf| + 0.2f) 2^-16, all in f32.  Every rounding
+    // between q and the union's test (T*T, the root, - 0.1f, - s) is monotone and within
+    // 2^-24 of values of magnitude <= |nsdf| + 0.22 near the threshold, against a margin of
+    // 2^-16 (|nsdf| + 0.2) -- sixty-fold; 0.11f - 0.1f falls short of 0.01f by 2e-9 of it.  With
+    // T <= 0 every sphere passes (d >= -0.1f and -nsdf >= 0.11 + margin).  A NaN nsdf gives a NaN
+    // T2 and the exact path.  A far sphere adds +0 to s (fmaf(d, 0, s) with d > 0 whenever s is
+    // +-0), so neither its root nor d is formed: one compare per sphere instead of v_sqrt_f32
+    // and five VALU.  tests/test_oracle.py::test_scene_far_screen_implies_union_test samples the
+    // implication at and around the threshold.
     if (__ballot(!(lo >= 0x1p-96f && hi <= 0x1.fffffep127f)) == 0) {
+        const float T = __builtin_fmaf(__builtin_fabsf(nsdf) + 0.2f, 0x1p-16f, nsdf + 0.11f);
+        const float Tc = T < 0.0f ? 0.0f : T;
+        const float T2 = Tc * Tc;
         float s = nsdf;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-            const float sa = __builtin_amdgcn_sqrtf(q[i]);
-            const float da = sa - 0.1f;
-            const bool far = da - nsdf >= 0.01f + (__builtin_fabsf(sa) + __builtin_fabsf(nsdf) + 0.01f) * 0x1p-18f;
-            if (__ballot(!far) == 0) s = __builtin_fmaf(da, 0.0f, s);
+            if (__ballot(!(q[i] >= T2)) == 0) s = s + 0.0f;
             else s = smooth_union(s, sqrt_rn_normal(q[i]) - 0.1f, 0.01f);
         }
         return s;

@@ -117,6 +117,34 @@ def test_smooth_union_kernel_form_bit_exact():
     assert same.all(), (d1[~same][:5], d2[~same][:5], ref[~same][:5], ker[~same][:5])
 
 
+def test_scene_far_screen_implies_union_test():
+    """nr_device.h many_sphere skips a sphere (adds +0 to the running union s) when its squared
+    distance q >= max(T, 0)^2, T = (nsdf + 0.11f) + (|nsdf| + 0.2f) 2^-16 in f32.  Sampled at and
+    just above the threshold, over surface values across scales, signed zeros and the T <= 0
+    edge: the reference's sdfOpSmoothUnion(s, sqrtf(q) - 0.1f, 0.01) (volumeRender_kernel.cu:
+    144-149, :189) equals s + 0 for s = nsdf, s below it, and s above it by far more than a
+    union's rounding (the running union never exceeds nsdf but for that)."""
+    rng = np.random.default_rng(12)
+    n = 400_000
+    f = np.float32
+    X = np.concatenate([rng.uniform(-1.5, 2.5, n), rng.uniform(-0.12, -0.10, n // 4),
+                        rng.standard_normal(n // 4) * rng.choice([1e-6, 1e-3, 1e2, 1e6], n // 4),
+                        [0.0, -0.0, -0.11, -0.1100001, 1e-30, -1e-30]]).astype(f)
+    T = ((np.abs(X) + f(0.2)).astype(np.float64) * 2.0 ** -16 + (X + f(0.11)).astype(np.float64)).astype(f)  # fmaf
+    T2 = np.where(T < 0, f(0), T).astype(f) ** 2
+    qs = [T2, np.nextafter(T2, f(np.inf)), np.nextafter(np.nextafter(T2, f(np.inf)), f(np.inf)),
+          (T2 * f(1.0 + 2 ** -20)).astype(f), (T2 * rng.uniform(1, 4, T2.size)).astype(f),
+          np.full_like(T2, 0.0), np.full_like(T2, 1e-30)]
+    for q in qs:
+        far = q >= T2
+        d = (np.sqrt(q) - f(0.1)).astype(f)
+        for s in (X, (X - np.abs(X) * f(2 ** -10) - f(1e-4)).astype(f), (X + (np.abs(X) + f(0.01)) * f(2 ** -21)).astype(f)):
+            ref, _ = oracle.smooth_union_pair(s[far], d[far], 0.01)
+            want = (s[far] + f(0.0)).astype(f)
+            same = ref.view(np.uint32) == want.view(np.uint32)
+            assert same.all(), (X[far][~same][:5], q[far][~same][:5], s[far][~same][:5])
+
+
 def test_smooth_subtraction_kernel_form_bit_exact():
     """nr_device.h evaluates sdfOpSmoothSubtraction (volumeRender_kernel.cu:137-142) without
     the f64 division when |d1+d2| >= k (h exactly 0 or 1); bit-identical to the reference
