@@ -64,6 +64,20 @@ namespace nr {
 #ifndef NR_DENSE_GEN
 #define NR_DENSE_GEN 1
 #endif
+// Bulk generation's queue reservations (round 3): up to two ranges per generation (what is
+// left of the wave's pool + the pending reservation), chunks of NR_QUEUE_CHUNK_DENSE positions
+// requested whenever the pool holds fewer than that -- launches of >= 4 frames; launches of
+// fewer take chunks of NR_QUEUE_CHUNK_DENSE1, since positions a wave holds ahead lengthen a
+// single frame's tail (tools/ab_lowp.sh, profiles/r3_ab_experiments.txt (17)).
+#ifndef NR_QUEUE_TWO_RANGES
+#define NR_QUEUE_TWO_RANGES 1
+#endif
+#ifndef NR_QUEUE_CHUNK_DENSE
+#define NR_QUEUE_CHUNK_DENSE 64
+#endif
+#ifndef NR_QUEUE_CHUNK_DENSE1
+#define NR_QUEUE_CHUNK_DENSE1 32
+#endif
 // (fp32: A/B only -- its ring would cost the batched instance its fourth workgroup per CU)
 #ifndef NR_DENSE_GEN_FP32
 #define NR_DENSE_GEN_FP32 0
@@ -165,6 +179,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     // rays generated in bulk through an LDS buffer (NR_DENSE_GEN): the reduced-precision tracers
     constexpr bool DENSE = NR_DENSE_GEN && (PREC != NR_PRECISION_FP32 || NR_DENSE_GEN_FP32) && !PROBE;
+    constexpr bool TWO = DENSE && NR_QUEUE_TWO_RANGES;
+    // pool size; the next reservation is requested when the pool holds fewer than QLOW
+    const uint32_t QCHUNK = TWO ? (BATCH && T.nframes >= 4 ? NR_QUEUE_CHUNK_DENSE : NR_QUEUE_CHUNK_DENSE1) : NR_QUEUE_CHUNK;
+    const uint32_t QLOW = TWO ? QCHUNK : NR_QUEUE_LOW;
     __shared__ FrameLds sf[BATCH ? NR_MAX_BATCH : 1];
     if constexpr (BATCH) {
         for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // 18 words per FrameLds
@@ -213,7 +231,8 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                              // bool, so that the compiler keeps it in a VGPR, not a lane mask)
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
-    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene, step
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene,
+    // step; and within refill: queue reservation, bulk ray generation, dealing from the ring
     constexpr bool timing = STAMPS;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
@@ -260,12 +279,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                 const long tot = shard_total(shard);
                                 if ((long)b < tot) {
                                     pool_base = b;
-                                    pool_cnt = (uint32_t)min((long)NR_QUEUE_CHUNK, tot - (long)b);
+                                    pool_cnt = (uint32_t)min((long)QCHUNK, tot - (long)b);
                                 }
                             }
                             while (pool_cnt == 0) {  // nothing reserved: a blocking reservation
                                 const long tot = shard_total(shard);
-                                const uint32_t w = max(want, (uint32_t)NR_QUEUE_CHUNK);
+                                const uint32_t w = max(want, (uint32_t)QCHUNK);
                                 uint32_t b = 0;
                                 if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, w);
                                 b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);  // lane 0: the whole wave is active
@@ -288,8 +307,8 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             pool_base += got;
                             pool_cnt -= got;
                         }
-                        if (!qempty && !pend && pool_cnt < NR_QUEUE_LOW) {
-                            if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)NR_QUEUE_CHUNK);
+                        if (!qempty && !pend && pool_cnt < QLOW) {
+                            if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)QCHUNK);
                             pend = true;
                         }
                     } else {
@@ -360,16 +379,54 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                     // (a wave capped at T.take lanes buffers at most that many rays, so that a small
                     // launch's rays stay spread over the waves)
                     if (rb_n < nfree && !qempty) {
-                        uint32_t base = 0, got = 0;
-                        reserve((uint32_t)T.take - rb_n, base, got);
+                        uint32_t base = 0, got = 0, base2 = 0, got2 = 0;
+                        unsigned long long tsub = timing ? __builtin_amdgcn_s_memtime() : 0ull;
+                        const uint32_t want = (uint32_t)T.take - rb_n;
+                        if constexpr (QPF && TWO) {
+                            // Up to two ranges: what is left of the wave's pool, then the pending
+                            // reservation (requested a bulk generation earlier, so it is back by now)
+                            // -- a short pool remainder does not cut this generation short.
+                            if (pool_cnt) {
+                                base = pool_base;
+                                got = min(want, pool_cnt);
+                                pool_base += got;
+                                pool_cnt -= got;
+                            }
+                            if (got < want) {
+                                if (pend) {
+                                    const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend_v);
+                                    pend = false;
+                                    const long tot = shard_total(shard);
+                                    if ((long)b < tot) {
+                                        pool_base = b;
+                                        pool_cnt = (uint32_t)min((long)QCHUNK, tot - (long)b);
+                                    }
+                                }
+                                if (pool_cnt == 0 && got == 0) reserve(want, base, got);  // blocking
+                                else if (pool_cnt) {
+                                    base2 = pool_base;
+                                    got2 = min(want - got, pool_cnt);
+                                    pool_base += got2;
+                                    pool_cnt -= got2;
+                                }
+                            }
+                            if (!qempty && !pend && pool_cnt < QLOW) {
+                                if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)QCHUNK);
+                                pend = true;
+                            }
+                        } else {
+                            reserve(want, base, got);
+                        }
+                        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[5] += t - tsub; tsub = t; }
                         bool hit = false, keep = false;
                         F3 gp = mk3(0.0f, 0.0f, 0.0f), gd = mk3(0.0f, 0.0f, 0.0f);
                         float gt = 0.0f;
                         uint32_t glp = 0;
                         int gf = 0;
-                        if ((uint32_t)lane < got) {
+                        if ((uint32_t)lane < got + got2) {
                             int px, py;
-                            if (pixel_of(base + (uint32_t)lane, gf, px, py)) {
+                            const uint32_t qpos = (uint32_t)lane < got ? base + (uint32_t)lane : base2 + ((uint32_t)lane - got);
+                            if (pixel_of(qpos, gf, px, py)) {
                                 glp = (uint32_t)((long)py * A.W + px);
                                 hit = gen_ray(A, T, BATCH ? sf[gf].inv_view : A.inv_view, px, py, gp, gd, gt);
                                 keep = hit && A.max_steps > 0;
@@ -385,9 +442,14 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             if constexpr (BATCH) rbuf_f[wid][slot] = (uint8_t)gf;
                         }
                         rb_n += (uint32_t)__popcll(km);
+                        if constexpr (timing) {
+                            __builtin_amdgcn_s_waitcnt(0);
+                            ph[6] += __builtin_amdgcn_s_memtime() - tsub;
+                        }
                     }
                     const uint32_t take = min(nfree, rb_n);
                     if (take) {
+                        const unsigned long long tsub = timing ? __builtin_amdgcn_s_memtime() : 0ull;
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                         const uint32_t rank = rank_below(freem);
                         if (it < 0 && rank < take) {
@@ -402,6 +464,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                         }
                         rb_head = (rb_head + take) & 63u;
                         rb_n -= take;
+                        if constexpr (timing) {
+                            __builtin_amdgcn_s_waitcnt(0);
+                            ph[7] += __builtin_amdgcn_s_memtime() - tsub;
+                        }
                     }
                 } else {
                     uint32_t base = 0, got = 0;
@@ -563,7 +629,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         unsigned long long *st = T.stamps + 16 * gwave;
         st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime();
         st[3] = ((unsigned long long)wit_tail << 32) | wit;
-        for (int i = 0; i < 5; ++i) st[4 + i] = ph[i];
+        for (int i = 0; i < 8; ++i) st[4 + i] = ph[i];
     }
     if (lane == 0) {
         if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);

@@ -192,7 +192,8 @@ int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
 int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
  * {start, pixel queue drained, end (100 MHz), (wave iterations after the drain << 32) |
- * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene, step, -};
+ * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene, step, and within
+ * refill (bf16/fp16 tracers) in the queue reservation, bulk ray generation and dealing, -};
  * nr_debug_stamps copies the last
  * frame's (16 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
  * schedule writes each hit pixel's iteration count instead of its colour.  Bit 6 =

@@ -59,6 +59,9 @@ ph = s[:, 4:9].astype(np.float64)
 tot = ph.sum(axis=1)
 print("phase share of wave cycles (refill, shading, MLP, scene, step), all waves:",
       np.round(ph.sum(axis=0) / tot.sum(), 3).tolist())
+sub = s[:, 9:12].astype(np.float64).sum(axis=0)
+print("within refill (reduced-precision tracers): reservation, bulk generation, dealing from the ring:",
+      np.round(sub / tot.sum(), 3).tolist())
 for i in last[-3:]:
     print(f"  wave ending {end[i]:.1f} us: cycles/iter refill {ph[i,0]/max(wit[i],1):.0f} shading {ph[i,1]/max(wit[i],1):.0f} "
           f"mlp {ph[i,2]/max(wit[i],1):.0f} scene {ph[i,3]/max(wit[i],1):.0f} step {ph[i,4]/max(wit[i],1):.0f}")
