@@ -231,7 +231,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                              // bool, so that the compiler keeps it in a VGPR, not a lane mask)
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
-    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tph = 0;  // stamps: cycles in refill, shading, MLP, scene,
+    unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tph = 0;
+    // after the queue drained: cycles in refill + shading + step, MLP, scene; iterations with <= 4 rays
+    unsigned long long pt[4] = {0, 0, 0, 0};  // stamps: cycles in refill, shading, MLP, scene,
     // step; and within refill: queue reservation, bulk ray generation, dealing from the ring
     constexpr bool timing = STAMPS;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         // Once the queue is drained a partial pass waits until the wave's last ray has
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
         // its size, and the marching rays must not wait for it.
-        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         uint64_t lm = __ballot(it >= 0);
         while (nstash >= 16 || (drained && nstash > 0 && !lm)) {
             const int nb = min(16, nstash);
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             nconv += (uint64_t)nb;
             nstash -= nb;
         }
-        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         if (!lm) {
             if (drained && nstash == 0) break;
             continue;
@@ -561,11 +563,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         // ---- MLP on every live point, then one sphere-trace step per ray
         if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
+        if constexpr (timing) pt[3] += (drained && __popcll(lm) <= 4) ? 1 : 0;
         if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
-            ph[2] += t - tph; tph = t;
+            ph[2] += t - tph; pt[1] += drained ? t - tph : 0; tph = t;
         }
         nsteps += (uint64_t)__popcll(lm);
         ++wit;
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             if constexpr (timing) {
                 __builtin_amdgcn_s_waitcnt(0);
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
-                ph[3] += t - tph; tph = t;
+                ph[3] += t - tph; pt[2] += drained ? t - tph : 0; tph = t;
             }
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
@@ -615,7 +618,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)rf;
         }
         nstash += (int)__popcll(cm);
-        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; tph = t; }
+        if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         const bool h = __ballot(it >= 0 && it >= T.hold_age) != 0;
         if (h != hold) {
             hold = h;
@@ -630,6 +633,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime();
         st[3] = ((unsigned long long)wit_tail << 32) | wit;
         for (int i = 0; i < 8; ++i) st[4 + i] = ph[i];
+        for (int i = 0; i < 4; ++i) st[12 + i] = pt[i];
     }
     if (lane == 0) {
         if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);

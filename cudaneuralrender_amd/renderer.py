@@ -249,7 +249,8 @@ class Renderer:
         """Per-wave stamps of the last k_trace: {start, queue drained, end (100 MHz ticks),
         iterations after drain << 32 | iterations, shader-clock cycles in refill, shading,
         MLP, scene, step, within refill: reservation, bulk generation, dealing (bf16/fp16),
-        4 x reserved}."""
+        after the drain: cycles in refill + shading + step, MLP, scene, and iterations with at
+        most 4 rays}."""
         n = ctypes.c_size_t()
         self._chk(self._L.nr_debug_stamps(self._ctx, None, 0, ctypes.byref(n)))
         buf = np.zeros((n.value, 16), np.uint64)

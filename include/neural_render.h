@@ -193,14 +193,17 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
  * {start, pixel queue drained, end (100 MHz), (wave iterations after the drain << 32) |
  * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene, step, and within
- * refill (bf16/fp16 tracers) in the queue reservation, bulk ray generation and dealing, -};
+ * refill (bf16/fp16 tracers) in the queue reservation, bulk ray generation and dealing; after
+ * the queue drained: cycles in refill + shading + step, MLP, scene, iterations with at most
+ * 4 rays};
  * nr_debug_stamps copies the last
  * frame's (16 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
  * schedule writes each hit pixel's iteration count instead of its colour.  Bit 6 =
  * MLP latency probe: nr_mlp_forward(X >= 64 points, Y >= 65 floats, n = repetitions, on
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
  * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
- * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
+ * layer, bit 12 times the tail's one-ray-per-row VALU form (row r evaluates X[r], its value
+ * in Y[1 + 16 r]).  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
  * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = the plain ReLU
  * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
  * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and

@@ -27,6 +27,9 @@ ap.add_argument("--temporal", type=int, default=0, help="nr_set_temporal_order")
 ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (1024: frame-major batch queue)")
 ap.add_argument("--hold", type=int, default=0, help="nr_set_age_hold age (0: off)")
 ap.add_argument("--band", type=int, default=1, help="rows per band dealt round-robin (bench.py BAND)")
+ap.add_argument("--single", action="store_true",
+                help="time one-frame launches through nr_render_shard (the one-frame k_trace instance) "
+                     "instead of nr_render_batch")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 iv, nm = nr.camera(0, 0, 2)
@@ -44,13 +47,18 @@ for n in (int(x) for x in a.shards.split(",")):
     for b in (int(x) for x in a.batches.split(",")):
         cams = [(iv, nm, 0)] * b
         ptrs = [t.data_ptr() for t in bufs[:b]]
+        def launch():
+            if a.single and b == 1:
+                r.render_shard_device(ptrs[0], S, S, a.band, n, 0, a.steps)
+            else:
+                r.render_batch_device(ptrs, S, S, cams, a.steps, a.band, n, 0)
         for _ in range(2):
-            r.render_batch_device(ptrs, S, S, cams, a.steps, a.band, n, 0)
+            launch()
         r.synchronize()
         t0 = time.perf_counter()
         for _ in range(max(1, a.frames // b)):
-            r.render_batch_device(ptrs, S, S, cams, a.steps, a.band, n, 0)
+            launch()
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
-        line.append(f"batch {b}: {dt:.3f} ms/frame")
+        line.append(f"{'single' if a.single and b == 1 else 'batch'} {b}: {dt:.3f} ms/frame")
     print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} debug {a.debug} band {a.band} hold {a.hold}: " + "  ".join(line), flush=True)

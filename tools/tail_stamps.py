@@ -65,3 +65,10 @@ print("within refill (reduced-precision tracers): reservation, bulk generation, 
 for i in last[-3:]:
     print(f"  wave ending {end[i]:.1f} us: cycles/iter refill {ph[i,0]/max(wit[i],1):.0f} shading {ph[i,1]/max(wit[i],1):.0f} "
           f"mlp {ph[i,2]/max(wit[i],1):.0f} scene {ph[i,3]/max(wit[i],1):.0f} step {ph[i,4]/max(wit[i],1):.0f}")
+tl = s[:, 12:15].astype(np.float64)
+wt = np.maximum(wit_tail, 1)
+print("after the drain, all waves: cycles per tail iteration refill+shading+step / MLP / scene:",
+      np.round(tl.sum(axis=0) / wt.sum(), 0).tolist(), f" iterations with <= 4 rays: {int(s[:, 15].sum())} of {int(wit_tail.sum())}")
+for i in last[-3:]:
+    print(f"  wave ending {end[i]:.1f} us: tail cycles/iter other {tl[i,0]/wt[i]:.0f} mlp {tl[i,1]/wt[i]:.0f} scene {tl[i,2]/wt[i]:.0f}; "
+          f"iterations with <= 4 rays {int(s[i, 15])} of {int(wit_tail[i])}")
