@@ -19,9 +19,9 @@ for s in $STEPS; do
     prof) timeout -k 10 900 bash tools/profile_round.sh $TAG > $O/profile_round_$TAG.log 2>&1 ;;
     mlp) timeout -k 10 300 python -u tools/mlp_bench.py --n 16777216 --iters 10 --precision fp32,bf16,fp16,fp32x3 --bpc 8,12 > $O/mlp_$TAG.log 2>&1 ;;
     cfg) timeout -k 10 400 python -u tools/config_bench.py --frames 5 > $O/cfg_$TAG.log 2>&1 ;;
-    pmc_bf16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16_$TAG bf16 8 > $O/pmc_bf16_$TAG.txt 2>&1 ;;
-    pmc_fp16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_fp16_$TAG fp16 8 > $O/pmc_fp16_$TAG.txt 2>&1 ;;
-    pmc_x3) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_x3_$TAG fp32x3 8 > $O/pmc_x3_$TAG.txt 2>&1 ;;
+    pmc_bf16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16_$TAG bf16 12 > $O/pmc_bf16_$TAG.txt 2>&1 ;;
+    pmc_fp16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_fp16_$TAG fp16 12 > $O/pmc_fp16_$TAG.txt 2>&1 ;;
+    pmc_x3) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_x3_$TAG fp32x3 12 > $O/pmc_x3_$TAG.txt 2>&1 ;;
     march) timeout -k 10 400 bash tools/march_traffic.sh $O/march_$TAG 8 > $O/march_$TAG.json 2> $O/march_$TAG.err ;;
     bench) timeout -k 10 300 python -u bench.py $BENCH_ARGS > $O/bench_$TAG.json 2> $O/bench_$TAG.err ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
