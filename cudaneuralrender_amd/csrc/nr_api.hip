@@ -978,18 +978,19 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
 
 // Queue positions are uint32 (pix_ctr atomics in k_trace): one launch hands out
 // shard_total = blocks of the busiest queue shard x 64 x frames positions.  Past a shard's end
-// each wave can hold one pending reservation (NR_QUEUE_CHUNK = 32, the low-precision tracers'
-// queue prefetch) and make one blocking reservation of up to 64 before it moves on: with the
-// grid nr_set_occupancy allows (16 workgroups x 4 waves per CU) on up to 512 CUs the
-// over-reservation stays below 512 x 16 x 4 x 96 = 3,145,728 (the old 2^19 assumed
-// 8 workgroups and no pending reservation).
+// a wave of the low-precision tracers can take two pending reservations of up to 64 positions
+// (NR_QUEUE_CHUNK_DENSE: one absorbed and found past the end while the wave still had positions
+// of its pool, the next requested right after) and one blocking reservation of up to 64 before
+// it moves on: with the grid nr_set_occupancy allows (16 workgroups x 4 waves per CU) on up to
+// 512 CUs the over-reservation stays below 512 x 16 x 4 x 192 = 6,291,456 (the old
+// 2^19 assumed 8 workgroups and no pending reservation).
 int nr_batch_frames_per_launch(int W, int H, int band, int nshards, int shard, int nframes, int queue_shards) {
     if (W < 1 || H < 1 || nframes < 1 || queue_shards < 1) return 0;
     const int rows = nr_shard_rows(H, band, nshards, shard);
     if (rows < 1) return std::min(nframes, NR_MAX_BATCH);
     const long long nblocks = (long long)((W + 7) / 8) * ((rows + 7) / 8);
     const long long per_frame = ((nblocks + queue_shards - 1) / queue_shards) * 64;  // busiest shard
-    const long long slop = 512ll * 16 * 4 * (64 + 32);
+    const long long slop = 512ll * 16 * 4 * (64 + 2 * 64);
     const long long cap = ((1ll << 32) - 1 - slop) / per_frame;
     return (int)std::min<long long>(std::min(nframes, NR_MAX_BATCH), cap);
 }
