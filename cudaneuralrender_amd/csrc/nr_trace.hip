@@ -199,7 +199,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     __shared__ float4 stash[4][STASH];
     __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
     // DENSE: per wave a ring of 64 generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame): 8.25 KB
-    __shared__ float4 rbuf[DENSE ? 4 : 1][DENSE ? 64 : 1][2];
+    // (two arrays of 16-byte entries: consecutive lanes' ds_write_b128 / ds_read_b128 stay
+    // conflict-free)
+    __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? 64 : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? 64 : 1];
     __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? 64 : 1];
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
@@ -439,8 +441,8 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                         const uint64_t km = __ballot(keep);
                         if (keep) {
                             const uint32_t slot = (rb_head + rb_n + rank_below(km)) & 63u;
-                            rbuf[wid][slot][0] = make_float4(gp.x, gp.y, gp.z, gt);
-                            rbuf[wid][slot][1] = make_float4(gd.x, gd.y, gd.z, __uint_as_float(glp));
+                            rbuf_p[wid][slot] = make_float4(gp.x, gp.y, gp.z, gt);
+                            rbuf_d[wid][slot] = make_float4(gd.x, gd.y, gd.z, __uint_as_float(glp));
                             if constexpr (BATCH) rbuf_f[wid][slot] = (uint8_t)gf;
                         }
                         rb_n += (uint32_t)__popcll(km);
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                         const uint32_t rank = rank_below(freem);
                         if (it < 0 && rank < take) {
                             const uint32_t slot = (rb_head + rank) & 63u;
-                            const float4 ra = rbuf[wid][slot][0], rd = rbuf[wid][slot][1];
+                            const float4 ra = rbuf_p[wid][slot], rd = rbuf_d[wid][slot];
                             p = mk3(ra.x, ra.y, ra.z);
                             tfar = ra.w;
                             d = mk3(rd.x, rd.y, rd.z);
