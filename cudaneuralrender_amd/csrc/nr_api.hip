@@ -58,7 +58,7 @@ struct nr_ctx {
     int hold_age = 0, hold_prio = 2;
     int spread = -1;  // nr_set_pixel_spread; -1 = auto (spread_for)
     int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
-    int wave_rays = 64;  // nr_set_wave_rays
+    int wave_rays = 0;  // nr_set_wave_rays (0: automatic, wave_rays_for)
     int nq_shift = 3;    // nr_set_queue_shards: 8
     // nr_render_batch: per-frame arguments (pinned staging + device copy), host-output scratch
     FrameArgs *h_frames = nullptr, *d_frames = nullptr;
@@ -335,6 +335,17 @@ int default_bpc(const nr_ctx *c, size_t total, int nframes) {
     }
     if (total < M) return 2;
     return total < 2 * M ? 3 : 4;
+}
+
+// Rays per wave of a persistent launch (nr_set_wave_rays; 0 = automatic): an fp32 launch whose
+// pixels fill at most 1.5x its waves' 64-ray slots marches 32 per wave -- at 64 every ray is
+// dealt in the first refill and every wave runs 4 tiles per iteration (one 1024^2 frame on 8
+// row-band shards: 1.015 -> 0.854 ms; on 4 shards, 2 shards or whole frames 32 is neutral or
+// slower, and bf16, whose tiles are cheap, gains nothing; profiles/r3_ab_experiments.txt (24)).
+int wave_rays_for(const nr_ctx *c, size_t pixels, int grid) {
+    if (c->wave_rays > 0) return c->wave_rays;
+    if (c->precision == NR_PRECISION_FP32 && 2 * pixels <= 3 * (size_t)grid * 4 * 64) return 32;
+    return 64;
 }
 
 // Block-cost buffers of the temporal order / cost probe for a frame-shard shape: a new shape
@@ -905,8 +916,6 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     }
     T.inv_bw = 1.0 / (double)T.bw;
     T.inv_band = 1.0 / (double)band;
-    T.take = c->wave_rays;
-    T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
     const int cus = num_cus(c->device);
     // temporal block order (nr_set_temporal_order): every launch dispenses the blocks of its
     // frames longest-first by the costs the previous launch of this frame-shard shape recorded
@@ -934,6 +943,8 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix * n, n);
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
+        T.take = wave_rays_for(c, npix * n, grid);
+        T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
         if (c->temporal) {
             T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
             T.bcost = c->d_bcost;
@@ -1063,8 +1074,6 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         }
         T.inv_bw = 1.0 / (double)T.bw;
         T.inv_band = 1.0 / (double)band;
-        T.take = c->wave_rays;
-        T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
         if (c->temporal || c->probe_steps > 0)
             if ((rc2 = order_buffers(c, W, H, band, nshards, shard, T.nblocks)) != NR_OK) return rc2;
         const bool probe = c->probe_steps > 0 && max_steps > 0 && !(c->temporal && c->order_valid);
@@ -1075,6 +1084,8 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix, 1);
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
+        T.take = wave_rays_for(c, npix, grid);
+        T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
         if (c->debug & 1) {
             if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 16 * 8));
             T.stamps = c->d_stamps;
@@ -1337,7 +1348,7 @@ int nr_set_queue_shards(nr_ctx *c, int n) {
 }
 
 int nr_set_wave_rays(nr_ctx *c, int rays) {
-    if (!c || rays < 1 || rays > 64) return set_err(c, NR_E_INVALID, "nr_set_wave_rays: rays must be in [1, 64]");
+    if (!c || rays < 0 || rays > 64) return set_err(c, NR_E_INVALID, "nr_set_wave_rays: rays must be in [0, 64]");
     c->wave_rays = rays;
     return NR_OK;
 }

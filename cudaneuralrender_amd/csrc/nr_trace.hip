@@ -201,8 +201,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // DENSE: per wave a ring of 64 generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame): 8.25 KB
     // (two arrays of 16-byte entries: consecutive lanes' ds_write_b128 / ds_read_b128 stay
     // conflict-free)
-    __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? 64 : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? 64 : 1];
-    __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? 64 : 1];
+    // (the fp32 tracer's ring, when built, holds 16: its 4 workgroups per CU have 2 KB of LDS
+    // left each)
+    constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : 64;
+    __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? RB : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? RB : 1];
+    __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? RB : 1];
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -382,10 +385,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                     // rays from the buffer in order.
                     // (a wave capped at T.take lanes buffers at most that many rays, so that a small
                     // launch's rays stay spread over the waves)
-                    if (rb_n < nfree && !qempty) {
+                    if (rb_n < nfree && rb_n < (uint32_t)min(T.take, RB) && !qempty) {
                         uint32_t base = 0, got = 0, base2 = 0, got2 = 0;
                         unsigned long long tsub = timing ? __builtin_amdgcn_s_memtime() : 0ull;
-                        const uint32_t want = (uint32_t)T.take - rb_n;
+                        const uint32_t want = (uint32_t)min(T.take, RB) - rb_n;
                         if constexpr (QPF && TWO) {
                             // Up to two ranges: what is left of the wave's pool, then the pending
                             // reservation (requested a bulk generation earlier, so it is back by now)
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                         nhit += (uint64_t)__popcll(__ballot(hit));
                         const uint64_t km = __ballot(keep);
                         if (keep) {
-                            const uint32_t slot = (rb_head + rb_n + rank_below(km)) & 63u;
+                            const uint32_t slot = (rb_head + rb_n + rank_below(km)) & (uint32_t)(RB - 1);
                             rbuf_p[wid][slot] = make_float4(gp.x, gp.y, gp.z, gt);
                             rbuf_d[wid][slot] = make_float4(gd.x, gd.y, gd.z, __uint_as_float(glp));
                             if constexpr (BATCH) rbuf_f[wid][slot] = (uint8_t)gf;
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                         const uint32_t rank = rank_below(freem);
                         if (it < 0 && rank < take) {
-                            const uint32_t slot = (rb_head + rank) & 63u;
+                            const uint32_t slot = (rb_head + rank) & (uint32_t)(RB - 1);
                             const float4 ra = rbuf_p[wid][slot], rd = rbuf_d[wid][slot];
                             p = mk3(ra.x, ra.y, ra.z);
                             tfar = ra.w;
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             if constexpr (BATCH) rf = (int)rbuf_f[wid][slot];
                             it = 0;
                         }
-                        rb_head = (rb_head + take) & 63u;
+                        rb_head = (rb_head + take) & (uint32_t)(RB - 1);
                         rb_n -= take;
                         if constexpr (timing) {
                             __builtin_amdgcn_s_waitcnt(0);

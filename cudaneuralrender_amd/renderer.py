@@ -223,7 +223,8 @@ class Renderer:
         return self
 
     def set_wave_rays(self, rays):
-        """Persistent schedule: at most `rays` (1-64) rays per wave at once."""
+        """Persistent schedule: at most `rays` (1-64) rays per wave at once; 0 = automatic (the
+        default: 64, or 32 for an fp32 launch whose pixels fill at most 1.5x its waves' slots)."""
         self._chk(self._L.nr_set_wave_rays(self._ctx, int(rays)))
         return self
 

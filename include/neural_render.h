@@ -217,10 +217,12 @@ int nr_set_debug(nr_ctx *ctx, int flags);
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
-/* Rays per wave (persistent schedule, 1-64, default 64): a wave marches at most this
- * many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or two
- * 16-ray tiles -- shorter per-iteration latency for small frames or shards, where the
- * longest ray rather than the matrix-core throughput sets the frame time. */
+/* Rays per wave (persistent schedule, 1-64; 0 = automatic, the default): a wave marches at
+ * most this many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or
+ * two 16-ray tiles -- shorter per-iteration latency for small frames or shards, where the
+ * longest ray rather than the matrix-core throughput sets the frame time.  Automatic: 64, or
+ * 32 for an fp32 launch whose pixels fill at most 1.5x its waves' 64-ray slots (a frame on 8
+ * shards). */
 int nr_set_wave_rays(nr_ctx *ctx, int rays);
 /* Pixel-queue shards (persistent schedule; power of two <= 64, default 8): the queue's
  * atomic counters, each on its own 128-byte line, that the waves take pixels from. */

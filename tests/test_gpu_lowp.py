@@ -150,4 +150,4 @@ def test_lowp_ragged_frames_schedules_agree(rend, nets, chrome, prec):
                 assert all(np.array_equal(x, y) for x, y in zip(imgs, bref)), (W, H, steps, rays)
                 assert bst["ray_steps"] == bsref["ray_steps"], (W, H, steps, rays)
     finally:
-        rend.set_wave_rays(64).set_schedule("persistent").set_precision("fp32").set_view(*nr.camera(0, 0, 2), 0)
+        rend.set_wave_rays(0).set_schedule("persistent").set_precision("fp32").set_view(*nr.camera(0, 0, 2), 0)

@@ -329,8 +329,23 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
             assert np.array_equal(img, ref), (spread, age, prio, bpc)
             for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
                 assert st[k] == sref[k], (k, spread, age, prio, bpc)
-    finally:
+        # rays per wave: explicit 64 / 32 and automatic (0: 32 for an fp32 launch of at most 1.5x
+        # its waves' slots, this frame on 8 shards)
         rend.set_pixel_spread(-1).set_age_hold(0, 2).set_occupancy(0)
+        for rays in (64, 32, 0):
+            rend.set_wave_rays(rays)
+            img, st = rend.render(W, H, 128)
+            assert np.array_equal(img, ref) and st["ray_steps"] == sref["ray_steps"], rays
+            a8 = [rend.render_shard(W, H, 1, 8, k, 128)[0] for k in (0, 7)]
+            rend.set_wave_rays(64)
+            b8 = [rend.render_shard(W, H, 1, 8, k, 128)[0] for k in (0, 7)]
+            assert all(np.array_equal(x, y) for x, y in zip(a8, b8)), rays
+        with pytest.raises(nr.NRError):
+            rend.set_wave_rays(65)
+        with pytest.raises(nr.NRError):
+            rend.set_wave_rays(-1)
+    finally:
+        rend.set_pixel_spread(-1).set_age_hold(0, 2).set_occupancy(0).set_wave_rays(0)
 
 
 def test_iteration_map(rend, nets, chrome):

@@ -15,7 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=64)
 ap.add_argument("--batches", default="1,4,16,32")
 ap.add_argument("--bpc", type=int, default=0)
-ap.add_argument("--rays", type=int, default=64)
+ap.add_argument("--rays", type=int, default=0, help="nr_set_wave_rays (0: automatic)")
 ap.add_argument("--schedule", default="persistent")
 ap.add_argument("--shards", default="1,2,4,8")
 ap.add_argument("--precision", default="fp32")

@@ -21,7 +21,7 @@ ap.add_argument("--temporal", type=int, default=0)
 ap.add_argument("--spread", type=int, default=0)
 ap.add_argument("--hold", type=int, default=0)
 ap.add_argument("--nshards", type=int, default=1)
-ap.add_argument("--rays", type=int, default=64)
+ap.add_argument("--rays", type=int, default=0)
 ap.add_argument("--queues", type=int, default=8)
 a = ap.parse_args()
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
