@@ -338,13 +338,14 @@ int default_bpc(const nr_ctx *c, size_t total, int nframes) {
 }
 
 // Rays per wave of a persistent launch (nr_set_wave_rays; 0 = automatic): an fp32 launch whose
-// pixels fill at most 1.5x its waves' 64-ray slots marches 32 per wave -- at 64 every ray is
-// dealt in the first refill and every wave runs 4 tiles per iteration (one 1024^2 frame on 8
-// row-band shards: 1.015 -> 0.854 ms; on 4 shards, 2 shards or whole frames 32 is neutral or
-// slower, and bf16, whose tiles are cheap, gains nothing; profiles/r3_ab_experiments.txt (24)).
+// pixels fill at most 2x its waves' 64-ray slots marches 32 per wave -- at 64 nearly every ray
+// is dealt in the first refills and every wave runs 4 tiles per iteration (one 1024^2 frame on
+// 8 row-band shards: 1.015 -> 0.854 ms, on 4 shards 1.139 -> 1.124; on 2 shards or whole frames
+// 32 is slower, and bf16, whose tiles are cheap, gains nothing; profiles/r3_ab_experiments.txt
+// (24), (25)).
 int wave_rays_for(const nr_ctx *c, size_t pixels, int grid) {
     if (c->wave_rays > 0) return c->wave_rays;
-    if (c->precision == NR_PRECISION_FP32 && 2 * pixels <= 3 * (size_t)grid * 4 * 64) return 32;
+    if (c->precision == NR_PRECISION_FP32 && pixels <= 2 * (size_t)grid * 4 * 64) return 32;
     return 64;
 }
 

@@ -224,7 +224,7 @@ class Renderer:
 
     def set_wave_rays(self, rays):
         """Persistent schedule: at most `rays` (1-64) rays per wave at once; 0 = automatic (the
-        default: 64, or 32 for an fp32 launch whose pixels fill at most 1.5x its waves' slots)."""
+        default: 64, or 32 for an fp32 launch whose pixels fill at most 2x its waves' slots)."""
         self._chk(self._L.nr_set_wave_rays(self._ctx, int(rays)))
         return self
 

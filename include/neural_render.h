@@ -221,8 +221,8 @@ int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
  * most this many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or
  * two 16-ray tiles -- shorter per-iteration latency for small frames or shards, where the
  * longest ray rather than the matrix-core throughput sets the frame time.  Automatic: 64, or
- * 32 for an fp32 launch whose pixels fill at most 1.5x its waves' 64-ray slots (a frame on 8
- * shards). */
+ * 32 for an fp32 launch whose pixels fill at most 2x its waves' 64-ray slots (a frame on 4 or
+ * 8 shards). */
 int nr_set_wave_rays(nr_ctx *ctx, int rays);
 /* Pixel-queue shards (persistent schedule; power of two <= 64, default 8): the queue's
  * atomic counters, each on its own 128-byte line, that the waves take pixels from. */

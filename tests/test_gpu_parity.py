@@ -329,7 +329,7 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
             assert np.array_equal(img, ref), (spread, age, prio, bpc)
             for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
                 assert st[k] == sref[k], (k, spread, age, prio, bpc)
-        # rays per wave: explicit 64 / 32 and automatic (0: 32 for an fp32 launch of at most 1.5x
+        # rays per wave: explicit 64 / 32 and automatic (0: 32 for an fp32 launch of at most 2x
         # its waves' slots, this frame on 8 shards)
         rend.set_pixel_spread(-1).set_age_hold(0, 2).set_occupancy(0)
         for rays in (64, 32, 0):
