@@ -197,8 +197,10 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
     // the x values repeat in every row, so the 3 x, 3 y and 1 z coordinates are formed
-    // once with the same f64 operations and reused.
-    const float x0 = (float)((double)p.x + 0.5);
+    // once with the same f64 operations and reused -- but for x0: p.x + 0.5 is exact in f64 for
+    // |p.x| >= 2^-30 and rounds to 0.5 either way below, so the single f32 add gives the same
+    // bits (tests/test_oracle.py::test_scene_x0_f32_add_equals_f64_form).
+    const float x0 = p.x + 0.5f;
     const float x1 = (float)((double)x0 - 0.4);
     const float x2 = (float)((double)x1 - 0.4);
     const float ys = (float)((double)p.y - 0.6);
@@ -281,7 +283,7 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
 // manySphere(p, nSDF, false) (:176-196): the 9 spheres smooth-subtracted from the surface,
 // the coordinates formed as in many_sphere
 __device__ float many_sphere_sub(F3 p, float nsdf, double zoff) {
-    const float x0 = (float)((double)p.x + 0.5);
+    const float x0 = p.x + 0.5f;  // = (float)((double)p.x + 0.5), see many_sphere
     const float x1 = (float)((double)x0 - 0.4);
     const float x2 = (float)((double)x1 - 0.4);
     const float ys = (float)((double)p.y - 0.6);

@@ -117,6 +117,24 @@ def test_smooth_union_kernel_form_bit_exact():
     assert same.all(), (d1[~same][:5], d2[~same][:5], ref[~same][:5], ker[~same][:5])
 
 
+def test_scene_x0_f32_add_equals_f64_form():
+    """nr_device.h many_sphere forms the first sphere column's x as p.x + 0.5f; the reference's
+    cP.x = p.x + 0.5 (volumeRender_kernel.cu:186) promotes to f64 and stores to f32.  Equal bit
+    for bit on floats of every exponent, signed zeros, subnormals, infinities and NaN."""
+    rng = np.random.default_rng(21)
+    bits = rng.integers(0, 2 ** 32, 4_000_000, dtype=np.uint64).astype(np.uint32)
+    x = bits.view(np.float32)
+    near = (rng.uniform(-1, 1, 1_000_000) * 2.0 ** rng.integers(-40, 3, 1_000_000)).astype(np.float32)
+    sp = np.array([0.0, -0.0, 0.5, -0.5, -0.25, 2 ** -30, -2 ** -30, 2 ** -31, 1e-45, -1e-45, np.inf, -np.inf,
+                   np.nan, 16777216.0, -16777217.0, 3.4e38, -3.4e38], np.float32)
+    x = np.concatenate([x, near, sp])
+    with np.errstate(invalid="ignore", over="ignore"):
+        ref = (x.astype(np.float64) + 0.5).astype(np.float32)
+        ker = x + np.float32(0.5)
+    same = (ref.view(np.uint32) == ker.view(np.uint32)) | (np.isnan(ref) & np.isnan(ker))
+    assert same.all(), x[~same][:5]
+
+
 def test_scene_far_screen_implies_union_test():
     """nr_device.h many_sphere skips a sphere (adds +0 to the running union s) when its squared
     distance q >= max(T, 0)^2, T = (nsdf + 0.11f) + (|nsdf| + 0.2f) 2^-16 in f32.  Sampled at and
