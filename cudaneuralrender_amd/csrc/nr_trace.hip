@@ -198,11 +198,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // so that 4 fp32 workgroups share a CU
     __shared__ float4 stash[4][STASH];
     __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
-    // DENSE: per wave a ring of 64 generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame): 8.25 KB
-    // (two arrays of 16-byte entries: consecutive lanes' ds_write_b128 / ds_read_b128 stay
-    // conflict-free)
-    // (the fp32 tracer's ring, when built, holds 16: its 4 workgroups per CU have 2 KB of LDS
-    // left each)
+    // DENSE: per wave a ring of RB generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame), as two
+    // arrays of 16-byte entries so that consecutive lanes' ds_write_b128 / ds_read_b128 stay
+    // conflict-free: 64 rays, 8.25 KB per workgroup (the fp32 tracer's ring, an A/B build option,
+    // holds 16: its 4 workgroups per CU have 2 KB of LDS left each)
     constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : 64;
     __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? RB : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? RB : 1];
     __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? RB : 1];
@@ -236,10 +235,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                              // bool, so that the compiler keeps it in a VGPR, not a lane mask)
     uint64_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
+    // stamps: cycles in refill, shading, MLP, scene, step; and within refill: queue reservation,
+    // bulk ray generation, dealing from the ring
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tph = 0;
     // after the queue drained: cycles in refill + shading + step, MLP, scene; iterations with <= 4 rays
-    unsigned long long pt[4] = {0, 0, 0, 0};  // stamps: cycles in refill, shading, MLP, scene,
-    // step; and within refill: queue reservation, bulk ray generation, dealing from the ring
+    unsigned long long pt[4] = {0, 0, 0, 0};
     constexpr bool timing = STAMPS;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                 if constexpr (DENSE) {
                     // Ray generation in bulk: when the buffer holds fewer rays than there are free
                     // slots, every lane of the wave generates the ray of one reserved position
-                    // (up to 64 - rb_n of them) -- instead of only the few lanes a refill frees,
+                    // (up to min(take, RB) - rb_n of them) -- instead of only the few lanes a refill frees,
                     // with the rest of the wave idle through initMarcher's divisions and square
                     // roots -- and the hits are appended to the wave's LDS ray buffer (a ring
                     // of 64); background pixels are written at once.  The free slots then take
