@@ -34,6 +34,17 @@ namespace nr {
 #ifndef NR_TRACE_BPC_WIDE
 #define NR_TRACE_BPC_WIDE 4
 #endif
+// the bf16/fp16 instances (A/B knobs: workgroups per CU their registers are allocated for, the
+// bulk-generation ring, rays per shading pass)
+#ifndef NR_TRACE_BPC_LOWP
+#define NR_TRACE_BPC_LOWP NR_TRACE_BPC_WIDE
+#endif
+#ifndef NR_RING_LOWP
+#define NR_RING_LOWP 64
+#endif
+#ifndef NR_SHADE_RAYS_LOWP
+#define NR_SHADE_RAYS_LOWP 16
+#endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
@@ -172,7 +183,8 @@ __device__ __forceinline__ void set_priority(int prio) {
 #endif
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
 __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
-                                  : (PREC != NR_PRECISION_FP32 || BATCH) ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
+                                  : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
+                                  : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
@@ -202,7 +214,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // arrays of 16-byte entries so that consecutive lanes' ds_write_b128 / ds_read_b128 stay
     // conflict-free: 64 rays, 8.25 KB per workgroup (the fp32 tracer's ring, an A/B build option,
     // holds 16: its 4 workgroups per CU have 2 KB of LDS left each)
-    constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : 64;
+    constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : NR_RING_LOWP;
     __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? RB : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? RB : 1];
     __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? RB : 1];
     const int lane = lane_id();
@@ -509,8 +521,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         // its size, and the marching rays must not wait for it.
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         uint64_t lm = __ballot(it >= 0);
-        while (nstash >= 16 || (drained && nstash > 0 && !lm)) {
-            const int nb = min(16, nstash);
+        constexpr int SHR = PREC == NR_PRECISION_FP32 ? 16 : NR_SHADE_RAYS_LOWP;  // rays per shading pass
+        while (nstash >= SHR || (drained && nstash > 0 && !lm)) {
+            const int nb = min(SHR, nstash);
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
