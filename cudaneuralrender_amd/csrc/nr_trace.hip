@@ -45,6 +45,11 @@ namespace nr {
 #ifndef NR_SHADE_RAYS_LOWP
 #define NR_SHADE_RAYS_LOWP 16
 #endif
+// the bulk-generating tracers keep each marching ray's direction and pixel in LDS (one float4
+// per lane, read back by the step) instead of four VGPRs live across the MLP
+#ifndef NR_RAY_D_LDS
+#define NR_RAY_D_LDS 1
+#endif
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
@@ -217,6 +222,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : NR_RING_LOWP;
     __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? RB : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? RB : 1];
     __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? RB : 1];
+    // each lane's marching ray {d.xyz, pixel} (DLDS): 4 KB per workgroup
+    constexpr bool DLDS = DENSE && NR_RAY_D_LDS;
+    __shared__ float4 ray_dp[DLDS ? 4 : 1][DLDS ? 64 : 1];
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -476,8 +484,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             const float4 ra = rbuf_p[wid][slot], rd = rbuf_d[wid][slot];
                             p = mk3(ra.x, ra.y, ra.z);
                             tfar = ra.w;
-                            d = mk3(rd.x, rd.y, rd.z);
-                            pix = __float_as_uint(rd.w);
+                            if constexpr (DLDS) {
+                                ray_dp[wid][lane] = rd;
+                            } else {
+                                d = mk3(rd.x, rd.y, rd.z);
+                                pix = __float_as_uint(rd.w);
+                            }
                             if constexpr (BATCH) rf = (int)rbuf_f[wid][slot];
                             it = 0;
                         }
@@ -568,9 +580,14 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             if (__popc(tmask) > need) {
                 const int src = select_bit(lm, lane < nl ? lane : 0);
                 p = mk3(__shfl(p.x, src), __shfl(p.y, src), __shfl(p.z, src));
-                d = mk3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+                if constexpr (DLDS) {
+                    const float4 dp = ray_dp[wid][lane];
+                    ray_dp[wid][lane] = make_float4(__shfl(dp.x, src), __shfl(dp.y, src), __shfl(dp.z, src), __shfl(dp.w, src));
+                } else {
+                    d = mk3(__shfl(d.x, src), __shfl(d.y, src), __shfl(d.z, src));
+                    pix = (uint32_t)__shfl((int)pix, src);
+                }
                 tfar = __shfl(tfar, src);
-                pix = (uint32_t)__shfl((int)pix, src);
                 if constexpr (BATCH) rf = __shfl(rf, src);
                 const int it_src = __shfl(it, src);
                 it = lane < nl ? it_src : -1;
@@ -598,6 +615,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                 __builtin_amdgcn_s_waitcnt(0);
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
                 ph[3] += t - tph; pt[2] += drained ? t - tph : 0; tph = t;
+            }
+            if constexpr (DLDS) {
+                const float4 dp = ray_dp[wid][lane];
+                d = mk3(dp.x, dp.y, dp.z);
+                pix = __float_as_uint(dp.w);
             }
             tfar -= ts;
             int used = 0;  // iterations this ray consumed, if it ends now
