@@ -253,7 +253,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     int rf = 0;  // the ray's frame (BATCH)
     int it = -1, maxit = 0;  // it: iterations of the slot's ray; -1: no ray (an int, not a
                              // bool, so that the compiler keeps it in a VGPR, not a lane mask)
-    uint64_t nsteps = 0, nhit = 0, nconv = 0;
+    // per-wave statistics in 32 bits (fewer scalar registers to spill): a wave's rays hit and shaded
+    // are at most its share of the launch's < 2^32 queue positions; its ray-steps can exceed that
+    // (x max_steps), so they are flushed to the launch's counter past 2^30
+    uint32_t nsteps = 0, nhit = 0, nconv = 0;
     uint32_t wit = 0, wit_tail = 0;  // wave iterations, those after the queue drained (stamps)
     // stamps: cycles in refill, shading, MLP, scene, step; and within refill: queue reservation,
     // bulk ray generation, dealing from the ring
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                 if (!keep) put(gf, glp, 0u);  // background (:335-339) or no iterations at all
                             }
                         }
-                        nhit += (uint64_t)__popcll(__ballot(hit));
+                        nhit += (uint32_t)__popcll(__ballot(hit));
                         const uint64_t km = __ballot(keep);
                         if (keep) {
                             const uint32_t slot = (rb_head + rb_n + rank_below(km)) & (uint32_t)(RB - 1);
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                 }
                             }
                         }
-                        nhit += (uint64_t)__popcll(__ballot(hit));
+                        nhit += (uint32_t)__popcll(__ballot(hit));
                     }
                 }
             }
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                          : A.normal;
                 put(sfr, pxl, shade_color(A, nmx, nrm, rd));
             }
-            nconv += (uint64_t)nb;
+            nconv += (uint32_t)nb;
             nstash -= nb;
         }
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
@@ -605,7 +608,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const unsigned long long t = __builtin_amdgcn_s_memtime();
             ph[2] += t - tph; pt[1] += drained ? t - tph : 0; tph = t;
         }
-        nsteps += (uint64_t)__popcll(lm);
+        nsteps += (uint32_t)__popcll(lm);
+        if (nsteps >= (1u << 30)) {
+            if (lane == 0) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
+            nsteps = 0;
+        }
         ++wit;
         wit_tail += drained ? 1u : 0u;
         bool conv = false;
