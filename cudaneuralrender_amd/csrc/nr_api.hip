@@ -45,6 +45,7 @@ struct nr_ctx {
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
+    bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
     bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
                             // on the same packs
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
@@ -237,6 +238,7 @@ int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>
     int f32_clamp = 0;
     c->fused = pack_fp32_16(c->dims, c->kernels, c->biases, pack16, &f32_clamp);
     c->mlp16 = MlpArgs{};
+    c->mlp16.lp_stream = !c->no_stream;
     c->f32_clamp_ok = c->fused && f32_clamp != 0;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;
     if (c->fused) {
@@ -1218,7 +1220,8 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 12;
         int grid = (int)std::min<long>((n + 255) / 256, (long)num_cus(c->device) * bpc);
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
-            HIPCHK(c, launch_mlp_latency(c->mlp16, dX, dY, (int)n, (c->wave_rays + 15) / 16, (c->debug >> 7) & 1, s));
+            HIPCHK(c, launch_mlp_latency(c->mlp16, c->precision, dX, dY, (int)n,
+                                         ((c->wave_rays > 0 ? c->wave_rays : 64) + 15) / 16, (c->debug >> 7) & 1, s));
         else
             HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, std::max(grid, 1), s));
     } else {
@@ -1364,6 +1367,8 @@ int nr_set_debug(nr_ctx *c, int flags) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
+    c->no_stream = (flags >> 11) & 1;
+    c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;
     return NR_OK;

@@ -29,6 +29,43 @@ __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__re
     Y[1 + lane] = v;
 }
 
+// The same for the 16-bit MLP on 128 points (k_mlp16's form, mlp32_lowp_128; 7 hidden layers):
+// PART 0 = the whole evaluation (the stream if M.lp_stream, else the builtin form), PART 1 = the
+// pipelined stream alone (nr_mlp16_asm.h), its outputs fed back as its inputs.  Y[0] = shader
+// cycles per 128-point evaluation.
+template <int PREC, int PART>
+__global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
+                                                       int reps) {
+    uint16_t *slp = reinterpret_cast<uint16_t *>(nr_smem_diag);
+    float *sfl = reinterpret_cast<float *>(nr_smem_diag + M.lp_bytes);
+    for (int i = threadIdx.x; i < M.lp_bytes / 16; i += blockDim.x)
+        reinterpret_cast<int4 *>(slp)[i] = reinterpret_cast<const int4 *>(M.lp)[i];
+    for (int i = threadIdx.x; i < M.lpf_bytes / 16; i += blockDim.x)
+        reinterpret_cast<int4 *>(sfl)[i] = reinterpret_cast<const int4 *>(M.lpf)[i];
+    __syncthreads();
+    const int lane = lane_id();
+    constexpr bool CL = PREC == NR_PRECISION_BF16;
+    float x[2] = {X[3 * lane], X[3 * lane + 3]}, y[2] = {X[3 * lane + 1], X[3 * lane + 4]};
+    float z[2] = {X[3 * lane + 2], X[3 * lane + 5]}, fr[2] = {0.0f, 0.0f}, v[2] = {0.0f, 0.0f};
+    u32x4 kk[4][2];
+    for (int t = 0; t < 4; ++t) kk[t][0] = (u32x4){__float_as_uint(x[0]), __float_as_uint(y[0]), 0u, 0u};
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < reps; ++r) {
+        if constexpr (PART == 0) {
+            const float xr[2] = {x[0] + v[0] * 1e-30f, x[1] + v[1] * 1e-30f};
+            mlp32_lowp_128<PREC, 7, CL>(slp, sfl, M.in0, 7, fr, xr, y, z, v, M.lp_stream != 0);
+        } else {
+            mlp7_x4_stream<PREC, CL>(slp, sfl, kk);
+            for (int t = 0; t < 4; ++t) kk[t][0] = kk[t][1] & 0x3f003f00u;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
+    Y[1 + lane] = PART == 0 ? v[0] + v[1] : __uint_as_float(kk[0][0][0] ^ kk[3][1][3]);
+}
+
 template <int PART>
 static void launch_lat(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st) {
     const int sm = M.pk_bytes;
@@ -38,7 +75,16 @@ static void launch_lat(const MlpArgs &M, const float *X, float *Y, int reps, int
     else hipLaunchKernelGGL((k_mlp_latency<4, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
 }
 
-hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, int part, hipStream_t st) {
+hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float *Y, int reps, int nt, int part,
+                              hipStream_t st) {
+    if (prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16) {
+        if (M.nh != 7 || M.in0 != 3 || !M.lp) return hipErrorInvalidValue;
+        const int sm = M.lp_bytes + M.lpf_bytes;
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(1), dim3(64), sm, st, M, X, Y, reps); };
+        if (prec == NR_PRECISION_BF16) part ? go(k_mlp_latency_lp<NR_PRECISION_BF16, 1>) : go(k_mlp_latency_lp<NR_PRECISION_BF16, 0>);
+        else part ? go(k_mlp_latency_lp<NR_PRECISION_FP16, 1>) : go(k_mlp_latency_lp<NR_PRECISION_FP16, 0>);
+        return hipGetLastError();
+    }
     if (part) launch_lat<1>(M, X, Y, reps, nt, st);
     else launch_lat<0>(M, X, Y, reps, nt, st);
     return hipGetLastError();

@@ -16,6 +16,8 @@ struct MlpArgs {
                             // inputs within LP_INPUT_BOUND; the launch clears it otherwise
     int f32_clamp;          // fp32 pack scaled for the clamped ReLU (pack_fp32_16): used by the
                             // waves whose inputs are all within F32_INPUT_BOUND
+    int lp_stream;          // 16-bit MLP as the pipelined streams of nr_mlp16_asm.h (7 hidden
+                            // layers); 0 (nr_set_debug bit 11): the builtin form, same values
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
@@ -125,7 +127,8 @@ hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float 
 hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
 hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
-hipError_t launch_mlp_latency(const MlpArgs &M, const float *X, float *Y, int reps, int nt, int part, hipStream_t st);
+hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float *Y, int reps, int nt, int part,
+                              hipStream_t st);
 hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int bw, int dilate, hipStream_t st);
 hipError_t launch_assemble(const uint32_t *src, size_t stride, uint32_t *dst, int W, int H, int band, int nshards,
                            hipStream_t st);

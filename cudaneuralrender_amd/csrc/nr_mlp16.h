@@ -14,6 +14,7 @@
 // reference dense layer as restated by the oracle (denseLayer.cu:126-176).
 #pragma once
 #include "nr_device.h"
+#include "nr_mlp16_asm.h"
 
 namespace nr {
 
@@ -561,13 +562,111 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
 #ifndef NR_LP_FINAL_MFMA
 #define NR_LP_FINAL_MFMA 0
 #endif
+// The pipelined stream (nr_mlp16_asm.h, tools/gen_mlp_asm.py) for the 7-hidden-layer networks:
+// 1 = on (MlpArgs::lp_stream, cleared by nr_set_debug bit 11, selects it at run time), 0 = never
+#ifndef NR_LP_STREAM
+#define NR_LP_STREAM 1
+#endif
+// A/B: issue priority NR_STREAM_PRIO outside the stream, 0 inside it (0 = no priority change)
+#ifndef NR_STREAM_PRIO
+#define NR_STREAM_PRIO 0
+#endif
+
+// LDS byte address of a pointer into shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// Input layer + 7 hidden layers + the final layer's operand conversion of four 32-point tiles as
+// one software-pipelined instruction stream: tile t + 1's conversions issue beside tile t's MFMAs
+// (the builtin form issues each layer's 8 MFMAs, then its 32 conversions).  In: k[t][0] = tile t's
+// input-layer B operand; out: k[t][s] = the ReLU'd 16-bit B operands of the final layer -- the
+// values relu_pack_tiles gives after hidden_layers, bit for bit (same instructions, same
+// operands).  Registers are pinned to the stream's (v0-v143, see the generated header).
+template <int PREC, bool CL>
+__device__ __forceinline__ void mlp7_x4_stream(const uint16_t *__restrict__ lp, const float *__restrict__ fl,
+                                               u32x4 (&k)[4][2]) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const int lane = lane_id();
+    const uint32_t va = lds_addr(lp) + 16u * (uint32_t)lane, vb = lds_addr(fl) + 64u * (uint32_t)(lane >> 5);
+    f32x16 c0, c1, c2, c3, bb0, bb1;
+    u32x8 ab0, ab1;
+#define NR_STREAM_OPERANDS                                                                                          \
+    : "+{v[64:67]}"(k[0][0]), "=&{v[68:71]}"(k[0][1]), "+{v[72:75]}"(k[1][0]), "=&{v[76:79]}"(k[1][1]),            \
+      "+{v[80:83]}"(k[2][0]), "=&{v[84:87]}"(k[2][1]), "+{v[88:91]}"(k[3][0]), "=&{v[92:95]}"(k[3][1]),            \
+      "=&{v[0:15]}"(c0), "=&{v[16:31]}"(c1), "=&{v[32:47]}"(c2), "=&{v[48:63]}"(c3), "=&{v[96:103]}"(ab0),         \
+      "=&{v[104:111]}"(ab1), "=&{v[112:127]}"(bb0), "=&{v[128:143]}"(bb1)                                          \
+    : [va] "v"(va), [vb] "v"(vb)                                                                                   \
+    : "memory"
+#if NR_STREAM_PRIO
+#define NR_SP_IN "s_setprio 0\n"
+#else
+#define NR_SP_IN ""
+#endif
+    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_SP_IN NR_HID7_BF16_CLAMP NR_STREAM_OPERANDS);
+    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_SP_IN NR_HID7_BF16_MAX NR_STREAM_OPERANDS);
+    else asm volatile(NR_SP_IN NR_HID7_F16_MAX NR_STREAM_OPERANDS);
+#undef NR_SP_IN
+#if NR_STREAM_PRIO
+    __builtin_amdgcn_s_setprio(NR_STREAM_PRIO);
+#endif
+#undef NR_STREAM_OPERANDS
+}
+
 template <int PREC, int NH, bool CL>
 __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh_rt, const float (&fr)[2], const float (&x)[2],
-                                               const float (&y)[2], const float (&z)[2], float (&out)[2]) {
+                                               const float (&y)[2], const float (&z)[2], float (&out)[2],
+                                               bool stream = false) {
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
+    if constexpr (NR_LP_STREAM && NH == 7 && !NR_LP_FINAL_MFMA) {
+        if (stream) {
+            u32x4 kk[4][2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                // the input layer's B operands exactly as below
+                const uint32_t p0 = cvt2<PREC>(x[s], y[s]);
+                const float dx = x[s] - lo16f<PREC>(p0), dy = y[s] - hi16f<PREC>(p0);
+                const uint32_t q = cvt2<PREC>(z[s], dx);
+                const uint32_t r = cvt2<PREC>(dy, z[s] - lo16f<PREC>(q));
+                uint32_t f = 0;
+                if (in0 == 4) {
+                    const uint32_t f0 = cvt2<PREC>(fr[s], 0.0f);
+                    f = cvt2<PREC>(fr[s], fr[s] - lo16f<PREC>(f0));
+                }
+                const uint32_t qf = (q & 0xffffu) | (f << 16);
+                const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
+                const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
+                const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
+                const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) kk[2 * s + t][0] = (u32x4){w0[t], w1[t], w2[t], w3[t]};
+            }
+            mlp7_x4_stream<PREC, CL>(lp, fl, kk);
+            const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(7));
+            const u32x4 wf[2] = {F4[h], F4[2 + h]};
+            const float bf = fl[32 + 32 * 7];
+            float zt[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                float a = 0.0f;
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) a = dot2<PREC>(kk[t][st][q], wf[st][q], a);
+                zt[t] = a;
+            }
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[2 * s]), __float_as_uint(zt[2 * s + 1]),
+                                                                false, false);
+                out[s] = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + bf;
+            }
+            return;
+        }
+    }
     f32x16 acc[4];
     {
         const v8 A = reinterpret_cast<const v8 *>(lp)[lane];
@@ -643,8 +742,8 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
 template <int PREC, bool CL>
 __device__ __forceinline__ void mlp128_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh, const float (&fr)[2], const float (&x)[2], const float (&y)[2],
-                                               const float (&z)[2], float (&out)[2]) {
-    if (nh == 7) mlp32_lowp_128<PREC, 7, CL>(lp, fl, in0, nh, fr, x, y, z, out);
+                                               const float (&z)[2], float (&out)[2], bool stream) {
+    if (nh == 7) mlp32_lowp_128<PREC, 7, CL>(lp, fl, in0, nh, fr, x, y, z, out, stream);
     else mlp32_lowp_128<PREC, 0, CL>(lp, fl, in0, nh, fr, x, y, z, out);
 }
 

@@ -690,6 +690,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     }
 }
 
+#ifndef NR_MLP16_PRIO
+#define NR_MLP16_PRIO 0
+#endif
 // waves per SIMD k_mlp16's registers target (<= 96 VGPRs at 5)
 #ifndef NR_MLP16_WPS
 #define NR_MLP16_WPS 5
@@ -722,6 +725,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     constexpr int in0 = IN0;
+    if constexpr (NR_MLP16_PRIO == 1 && PREC != NR_PRECISION_FP32) {
+        // A/B: static issue priority by the wave's slot on its SIMD (HW_ID.WAVE_ID), so that the
+        // co-resident waves do not march through their streams in step
+        set_priority((int)(__builtin_amdgcn_s_getreg((3 << 11) | 4) & 3u));
+    }
     M.in0 = IN0;
     const auto rx = buffer_of(X, (uint32_t)n * (uint32_t)in0 * 4u), ry = buffer_of(Y, (uint32_t)n * 4u);
     // point i's inputs (zeros past the end); the 4th is the frame for 4-input networks
@@ -735,22 +743,19 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         }
     };
     auto store = [&](uint32_t i, float v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, i * 4u, 0, 0); };
-    // the wave's chunk index is uniform (SGPRs)
-    const int wave = (int)blockIdx.x * (int)(blockDim.x >> 6) + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int waves = (int)gridDim.x * (int)(blockDim.x >> 6);
+    // the wave's chunk index is uniform (SGPRs); launch_mlp16 launches 256-thread workgroups (blockDim,
+    // read from the dispatch packet by a vector load, would put the indices in VGPRs)
+    const int wave = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
+    const int waves = __builtin_amdgcn_readfirstlane((int)gridDim.x * 4);
     if constexpr (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16) {
         // 128 points per wave and chunk: point base + lane and base + 64 + lane; a last chunk of
         // at most 64 points takes the 64-point form
+        // The loop takes only whole 128-point chunks, so that one path leads from the next chunk's
+        // input loads to their use: with the ragged chunk inside it, the merge of its one-store path
+        // made hipcc wait for this chunk's stores too (s_waitcnt vmcnt(0) on every chunk, a store's
+        // round trip to memory).  The ragged last chunk follows the loop, on the wave whose turn it is.
         const int stride2 = waves * 128;
-        float nx[2], ny[2], nz[2], nf[2];
-        int base = wave * 128;
-        load((uint32_t)(base + lane), nx[0], ny[0], nz[0], nf[0]);
-        load((uint32_t)(base + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
-        for (; base < n; base += stride2) {
-            base = __builtin_amdgcn_readfirstlane(base);  // uniform: SGPRs, scalar branches
-            const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
-            load((uint32_t)(base + stride2 + lane), nx[0], ny[0], nz[0], nf[0]);
-            load((uint32_t)(base + stride2 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+        auto run = [&](int base, const float (&x)[2], const float (&y)[2], const float (&z)[2], const float (&f)[2]) {
             const int rem = n - base;
             // the bf16 clamped pack's input bound (NaN is not within it)
             constexpr float XB = LP_INPUT_BOUND, FB = LP_INPUT_BOUND;
@@ -762,15 +767,54 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                 const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
                 store((uint32_t)(base + lane), mlp16(M, S.s32, S.slp, S.sfl, PREC, f[0], x[0], y[0], z[0], tmask,
                                                      M.lp_clamp && __ballot(!ok0) == 0));
-                continue;
+                return;
             }
             float v[2];
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!(ok0 && ok1)) == 0)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v);
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
             else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v);
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
             store((uint32_t)(base + lane), v[0]);
             store((uint32_t)(base + 64 + lane), v[1]);
+        };
+        const int nfull = n & ~127;
+        float nx[2], ny[2], nz[2], nf[2];
+        int base = wave * 128;
+        load((uint32_t)(base + lane), nx[0], ny[0], nz[0], nf[0]);
+        load((uint32_t)(base + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+        // One chunk: its inputs (requested one chunk ahead) -> the next chunk's request -> MLP ->
+        // stores.  The first chunk is peeled off the loop, so that the loop is entered with the
+        // memory operations in flight that it is re-entered with (a chunk's two loads, then the
+        // previous chunk's two stores): hipcc merges the entry's and the back edge's wait counts,
+        // and with no stores on the entry path it waited for the previous chunk's stores before
+        // every chunk (a store's round trip to memory per chunk).
+        auto body = [&]() {
+            base = __builtin_amdgcn_readfirstlane(base);  // uniform: SGPRs, scalar branches
+            const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
+            load((uint32_t)(base + stride2 + lane), nx[0], ny[0], nz[0], nf[0]);
+            load((uint32_t)(base + stride2 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+            float v[2];
+            constexpr float XB = LP_INPUT_BOUND, FB = LP_INPUT_BOUND;
+            const bool ok = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
+                            __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
+                            __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
+            if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+            else
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+            store((uint32_t)(base + lane), v[0]);
+            store((uint32_t)(base + 64 + lane), v[1]);
+        };
+        if (base < nfull) {
+            body();
+            for (base += stride2; base < nfull; base += stride2) body();
+        }
+        // the ragged last chunk (1-127 points): the wave the grid-stride order gives it
+        if (nfull < n && (nfull >> 7) % waves == wave) {
+            float x[2], y[2], z[2], f[2];
+            load((uint32_t)(nfull + lane), x[0], y[0], z[0], f[0]);
+            load((uint32_t)(nfull + 64 + lane), x[1], y[1], z[1], f[1]);
+            run(nfull, x, y, z, f);
         }
         return;
     }

@@ -207,7 +207,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
  * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and
  * A/B of the two forms); fp32x3 by the fp32 MLP for every wave (its fallback, bit-exact fp32).  Bit 10 = nr_render_batch deals its pixel queue frame after
- * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected). */
+ * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected).  Bit 11 = the
+ * bf16/fp16 MLP of 7-hidden-layer networks in its builtin-compiled form instead of the
+ * software-pipelined instruction streams (nr_mlp16_asm.h; the same values, for A/B and parity). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next

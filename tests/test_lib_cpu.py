@@ -239,7 +239,7 @@ def _regs(ops):
 
 
 def _parse(line):
-    """(address, mnemonic, dst regs, src regs) of one llvm-objdump -d line, or None"""
+    """(address, mnemonic, dst regs, src regs, MFMA SrcC regs) of one llvm-objdump -d line, or None"""
     m = re.match(r"\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-F]+):", line)
     if not m:
         return None
@@ -247,12 +247,20 @@ def _parse(line):
     parts = [p.strip() for p in re.split(r",(?![^\[]*\])", ops)] if ops else []
     dst = _regs(parts[0]) if parts and not mn.startswith(("s_", "ds_write", "global_store", "buffer_store")) else set()
     src = set().union(*[_regs(p) for p in parts[1:]]) if len(parts) > 1 else set()
-    return addr, mn, dst, src
+    srcc = _regs(parts[3]) if mn.startswith("v_mfma") and len(parts) > 3 else set()
+    return addr, mn, dst, src, srcc
 
 
 def _wait_states(mn, line):
     m = re.match(r"\s+s_nop\s+(?:0x)?([0-9a-f]+)", line)
     return int(m.group(1), 16) + 1 if m else 1
+
+
+# MFMA -> VALU distances (wait states; tools/gen_mlp_asm.py): a VALU read or write of a register a
+# v_mfma_f32_32x32x16 writes needs 12 (hipcc's own padding; 13 required here), a VALU write of a
+# register it reads as SrcC 16 and as SrcA/B 8 (conservative); within the window every older MFMA
+# of the path is checked too, unless a VALU read of its result (a 'touch') proves it complete.
+RAW_STATES, SRCC_WAR_STATES, SRCAB_WAR_STATES = 13, 16, 8
 
 
 def check_clamp_runs(lines):
@@ -265,7 +273,7 @@ def check_clamp_runs(lines):
     addr_ix = {x[0]: n for n, (_, x) in enumerate(ins)}
     preds = {n: ([n - 1] if n > 0 and ins[n - 1][1][1] not in ("s_branch", "s_endpgm") else [])
              for n in range(len(ins))}
-    for n, (ln, (addr, mn, _, _)) in enumerate(ins):
+    for n, (ln, (addr, mn, _, _, _)) in enumerate(ins):
         m = re.match(r"\s+s_(?:c)?branch\w*\s+(-?\d+)", ln)
         if m:
             off = int(m.group(1))
@@ -292,21 +300,30 @@ def check_clamp_runs(lines):
             if (k, W, read_since) in seen:
                 continue
             seen.add((k, W, read_since))
-            ln, (addr, mn, dst, src) = ins[k]
-            if mn.startswith("v_mfma") and (dst & (S | D) or src & D):
-                assert dst & read_since, f"{where}: MFMA at {addr:#x} ({W} wait states before) not touched"
-                continue  # the touched MFMA completed, and every MFMA of this path before it
+            ln, (addr, mn, dst, src, srcc) = ins[k]
+            if mn.startswith("v_mfma"):
+                if dst & read_since:
+                    continue  # touched: it completed, and every MFMA of this path before it
+                # distance to the first instruction of the run that touches each register involved
+                for q in range(i, j):
+                    qd, qs = ins[q][1][2], ins[q][1][3]
+                    need = RAW_STATES if dst & (qs | qd) else 0
+                    if src & qd:
+                        need = max(need, SRCC_WAR_STATES if srcc & qd else SRCAB_WAR_STATES)
+                    assert W + (q - i) >= need, f"{where}: MFMA at {addr:#x} ({W + q - i} wait states before) not touched"
             if mn.startswith("v_") and not mn.startswith("v_mfma"):
                 read_since = read_since | frozenset(src)
             W += _wait_states(mn, ln)
             if W < 24:
                 stack.extend((q, W, read_since) for q in preds[k])
-        # forward: first MFMA reading a result of the run
+        # forward: first MFMA reading a result of the run, counted from the run's last write of
+        # a register it reads
         W, k = 0, j
         while k < len(ins):
-            ln, (addr, mn, dst, src) = ins[k]
+            ln, (addr, mn, dst, src, _) = ins[k]
             if mn.startswith("v_mfma") and src & D:
-                assert W >= 2, f"{where}: MFMA {W} wait states after the run"
+                last = max(q for q in range(i, j) if ins[q][1][2] & src)
+                assert W + (j - 1 - last) >= 2, f"{where}: MFMA {W + j - 1 - last} wait states after the run"
                 break
             if mn.startswith(("s_branch", "s_cbranch", "s_endpgm")):
                 break
@@ -324,10 +341,11 @@ def test_bf16_clamp_conversions_are_hazard_free(tmp_path):
     states before the touch) and on the block's trailing s_nop 1 (a VALU write needs 2 wait
     states before an MFMA reads it).  Checked on the generated code of every instance:
       * on every path into each run of v_cvt_pk_bf16_f32 ... clamp (control flow followed
-        through branches and branch targets), the most recent MFMA that writes a register the run
-        reads, or reads or writes a register the run writes, is followed before the run by a VALU
-        read of its result (the touch); a path is followed until 24 wait states separate it from
-        the run (beyond every MFMA hazard window);
+        through branches and branch targets), every MFMA that writes a register the run reads,
+        or reads or writes a register the run writes, is either followed before the run by a VALU
+        read of its result (the touch) or far enough ahead of it (RAW_STATES / *_WAR_STATES: the
+        pipelined streams of nr_mlp16_asm.h, whose runs sit between MFMAs, rely on distance); a
+        path is followed until 24 wait states separate it from the run (beyond every window);
       * the first MFMA after the run that reads one of its results is >= 2 wait states after it."""
     import shutil
     import subprocess
@@ -355,3 +373,38 @@ def test_bf16_clamp_conversions_are_hazard_free(tmp_path):
                 assert "not touched" in str(e)
                 caught += 1
     assert runs > 0 and caught > 0
+
+
+def test_mlp_stream_header_is_current_and_hazard_checked():
+    """nr_mlp16_asm.h (the 16-bit MLP's pipelined instruction streams) is what
+    tools/gen_mlp_asm.py generates today, and the generator's hazard check accepts every stream
+    (it raises on a violation before writing or comparing)."""
+    import subprocess
+    import sys
+    gen = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gen_mlp_asm.py")
+    r = subprocess.run([sys.executable, gen, "--check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_mlp_stream_checker_rejects_hazards():
+    """The generator's checker catches each hazard class it guards (a stream edited to break it)."""
+    import importlib.util
+    gen = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gen_mlp_asm.py")
+    spec = importlib.util.spec_from_file_location("gen_mlp_asm", gen)
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    st = g.build("bf16", True)
+    ins = st.ins
+
+    def broken(edit):
+        s2 = g.Stream()
+        s2.ins = edit(list(ins))
+        with pytest.raises(AssertionError):
+            g.check(s2)
+
+    first_nop = next(i for i, x in enumerate(ins) if x[1] == "nop")
+    broken(lambda l: l[:first_nop] + l[first_nop + 1:])                          # MFMA -> VALU read too soon
+    first_wait = next(i for i, x in enumerate(ins) if x[1] == "wait")
+    broken(lambda l: l[:first_wait] + l[first_wait + 1:])                        # LDS data used before the wait
+    last_cvt = max(i for i, x in enumerate(ins) if x[1] == "valu")
+    broken(lambda l: l[:last_cvt - 20])                                          # MFMA still in flight at the exit

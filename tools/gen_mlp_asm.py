@@ -1,0 +1,239 @@
+"""Generates cudaneuralrender_amd/csrc/nr_mlp16_asm.h: the 16-bit MLP's hidden layers for four
+32-point tiles (128 points per wave, k_mlp16) as one software-pipelined instruction stream.
+
+Why: compiled from builtins, every hidden layer issued its 8 MFMAs back to
+back and then converted all four tiles' accumulators (32 v_cvt_pk) with no MFMA in flight, so a
+wave alone kept the matrix pipe ~55 % busy and the waves of a SIMD, sharing the pipe, fell into
+step.  Here the conversion of tile t + 1 runs in the shadow of tile t's two MFMAs, and the next
+layer's tile 0 in the shadow of tile 3's, so one wave alone keeps the pipe nearly full:
+
+    layer l:  M(l,0,0) C(l,1)s0  M(l,0,1) C(l,1)s1  M(l,1,0) C(l,2)s0 ...  M(l,3,0) C(l+1,0)s0  M(l,3,1) C(l+1,0)s1
+
+M(l,t,s) = v_mfma_f32_32x32x16_{bf16,f16} of layer l, tile t, k-step s (s = 0 takes the bias as
+its accumulator init, s = 1 the s = 0 result); C(l,t)s = the 4 v_cvt_pk (bf16: with the clamp bit
+that is the ReLU on the clamped pack; otherwise + v_pk_max_i16) that turn registers 8s..8s+7 of
+tile t's accumulator into the B operand of k-step s.  Every instruction and operand is the one the
+builtin form issues, so the outputs are bit-identical; only the order changes.
+
+The stream runs inside one inline-asm statement, so the compiler neither pads its hazards nor
+counts its LDS reads: this script places the operand reads (ds_read_b128 of the next layer's A
+operands and biases into the idle one of two register buffers, one layer ahead) and CHECKS every
+hazard of the stream before it writes the header (check()).  The registers are pinned
+("{v[a:b]}" constraints): accumulators v0-v63, B operands v64-v95, A operands v96-v111, biases
+v112-v143.
+
+Run:  python tools/gen_mlp_asm.py   (writes the header; the CPU test suite checks it is current)
+"""
+import os
+import sys
+
+NH = 7                       # hidden layers of the bundled networks (others take the builtin form)
+ACC = lambda t: 16 * t                     # accumulator of tile t: v[16t : 16t+15]
+KOP = lambda t, s: 64 + 8 * t + 4 * s      # B operand of tile t, k-step s: 4 registers
+AOP = lambda b, s: 96 + 8 * b + 4 * s      # A operand of buffer b, k-step s: 4 registers
+BIAS = lambda b: 112 + 16 * b              # bias (accumulator init) of buffer b: 16 registers
+
+# hazard distances (wait states = instructions issued between producer and consumer; s_nop N
+# counts N + 1).  MFMA_VALU_RAW: hipcc's own gfx950 padding of v_mfma_f32_32x32x16 -> VALU read
+# is 12 (nr_trace.hip disassembly: MFMA, s_nop 10, read); one more here as margin.  The WAR rows
+# are conservative (the ISA's 8-pass SrcC value is smaller).
+MFMA_VALU_RAW = 13
+VALU_MFMA_RAW = 3
+SRCC_WAR = 16
+SRCAB_WAR = 8
+
+
+class Stream:
+    def __init__(self):
+        self.ins = []   # (text, kind, reads, writes, states)
+
+    def add(self, text, kind, reads=(), writes=(), states=1):
+        self.ins.append((text, kind, tuple(reads), tuple(writes), states))
+
+
+def rng(a, n):
+    return range(a, a + n)
+
+
+def build(prec, clamp):
+    dt = "bf16" if prec == "bf16" else "f16"
+    st = Stream()
+
+    def mfma(buf, t, s, layer0=False):
+        d = ACC(t)
+        a = AOP(buf, 0) if layer0 else AOP(buf, s)
+        b = KOP(t, s)
+        c = BIAS(buf) if (layer0 or s == 0) else ACC(t)
+        st.add(f"v_mfma_f32_32x32x16_{dt} v[{d}:{d + 15}], v[{a}:{a + 3}], v[{b}:{b + 3}], v[{c}:{c + 15}]", "mfma",
+               reads=[("A", r) for r in rng(a, 4)] + [("B", r) for r in rng(b, 4)] + [("C", r) for r in rng(c, 16)],
+               writes=list(rng(d, 16)))
+
+    def conv(t, s):
+        for q in range(4):
+            src = ACC(t) + 8 * s + 2 * q
+            dst = KOP(t, s) + q
+            if prec == "bf16" and clamp:
+                st.add(f"v_cvt_pk_bf16_f32 v{dst}, v{src}, v{src + 1} clamp", "valu", reads=[src, src + 1], writes=[dst])
+            else:
+                cvt = "v_cvt_pk_bf16_f32" if prec == "bf16" else "v_cvt_pk_f16_f32"
+                st.add(f"{cvt} v{dst}, v{src}, v{src + 1}", "valu", reads=[src, src + 1], writes=[dst])
+                st.add(f"v_pk_max_i16 v{dst}, v{dst}, 0", "valu", reads=[dst], writes=[dst])
+
+    def load(dst, addr, off):
+        o = f" offset:{off}" if off else ""
+        st.add(f"ds_read_b128 v[{dst}:{dst + 3}], %[{addr}]{o}", "lds", writes=list(rng(dst, 4)))
+
+    def a_loads(buf, j):       # hidden layer j's A operands (both k-steps) into buffer buf
+        load(AOP(buf, 0), "va", 1024 + 2048 * j)
+        load(AOP(buf, 1), "va", 2048 + 2048 * j)
+
+    def b_load(buf, j, i):     # quarter i of hidden layer j's bias into buffer buf
+        load(BIAS(buf) + 4 * i, "vb", 128 + 128 * j + 16 * i)
+
+    wait = lambda: st.add("s_waitcnt lgkmcnt(0)", "wait")
+    # ---- layer 0 (buffer 0): its A operand (k-step-0 slot) and bias; the B operands are inputs
+    load(AOP(0, 0), "va", 0)
+    for i in range(4):
+        load(BIAS(0) + 4 * i, "vb", 16 * i)
+    wait()
+    mfma(0, 0, 0, layer0=True)
+    a_loads(1, 0)
+    mfma(0, 1, 0, layer0=True)
+    for i in range(4):
+        b_load(1, 0, i)
+    mfma(0, 2, 0, layer0=True)
+    mfma(0, 3, 0, layer0=True)
+    st.add("s_nop 3", "nop", states=4)
+    conv(0, 0)
+    conv(0, 1)
+    # ---- hidden layers l = 1..NH (hidden layer j = l - 1, buffer l % 2); the next layer's
+    # operands go to the other buffer once this layer's MFMAs no longer read the old ones there
+    for l in range(1, NH + 1):
+        buf, j, nxt = l % 2, l - 1, l < NH
+        wait()
+        for t in range(4):
+            for s in range(2):
+                mfma(buf, t, s)
+                conv(t + 1 if t < 3 else 0, s)   # tile t + 1 of this layer, or tile 0 of the next
+                if nxt:
+                    if (t, s) == (1, 0):
+                        a_loads(1 - buf, j + 1)
+                    elif (t, s) == (1, 1):
+                        b_load(1 - buf, j + 1, 0)
+                    elif (t, s) == (2, 0):
+                        b_load(1 - buf, j + 1, 1)
+                    elif (t, s) == (2, 1):
+                        b_load(1 - buf, j + 1, 2)
+                        b_load(1 - buf, j + 1, 3)
+    # ---- tail: the final layer's B operands of tiles 1-3 (tile 0's ran beside M(NH, 3, *))
+    for t in (1, 2, 3):
+        conv(t, 0)
+        conv(t, 1)
+    check(st)
+    return st
+
+
+def check(st):
+    """Verifies every hazard of the stream (raises on the first violation)."""
+    pos = []   # wait-state position of each instruction
+    p = 0
+    for ins in st.ins:
+        pos.append(p)
+        p += ins[4]
+    # the input B operands (k-step 0 slots) were written by the compiler's VALU just before the stream
+    last_w = {r: (-1, "valu") for t in range(4) for r in rng(KOP(t, 0), 4)}
+    last_r = {}      # reg -> list of (index, operand role) of MFMA reads since the last write
+    pending = set()  # regs with an LDS load not yet waited for
+    for i, (text, kind, reads, writes, _) in enumerate(st.ins):
+        if kind == "wait":
+            pending.clear()
+            continue
+        regs_read = [r if isinstance(r, int) else r[1] for r in reads]
+        for r in regs_read:
+            if r in pending:
+                raise AssertionError(f"{i}: {text}: reads v{r} before its LDS load is waited for")
+            if r in last_w:
+                wi, wk = last_w[r]
+                dist = pos[i] - (pos[wi] + st.ins[wi][4]) if wi >= 0 else pos[i]   # states in between
+                if wk == "mfma" and kind != "mfma" and dist < MFMA_VALU_RAW:
+                    raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after MFMA {wi}")
+                if wk == "valu" and kind == "mfma" and dist < VALU_MFMA_RAW:
+                    raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after VALU {wi}")
+                if wk == "mfma" and kind == "mfma":
+                    # only an exact accumulate chain (same registers as C) may follow an MFMA
+                    role = [x[0] for x in reads if x[1] == r][0]
+                    if role != "C":
+                        raise AssertionError(f"{i}: {text}: MFMA operand {role} v{r} written by MFMA {wi}")
+        for r in writes:
+            for (ri, role) in last_r.get(r, []):
+                dist = pos[i] - (pos[ri] + st.ins[ri][4])
+                need = SRCC_WAR if role == "C" else SRCAB_WAR
+                if kind != "mfma" and dist < need:
+                    raise AssertionError(f"{i}: {text}: writes v{r} {dist} states after MFMA {ri} read it as {role}")
+            if r in last_w and last_w[r][1] == "mfma" and kind != "mfma":
+                wi = last_w[r][0]
+                if pos[i] - (pos[wi] + st.ins[wi][4]) < MFMA_VALU_RAW:
+                    raise AssertionError(f"{i}: {text}: overwrites v{r} too soon after MFMA {wi}")
+        for r in writes:
+            last_w[r] = (i, kind)
+            last_r[r] = []
+            if kind == "lds":
+                pending.add(r)
+        if kind == "mfma":
+            for role, r in reads:
+                last_r.setdefault(r, []).append((i, role))
+    if pending:
+        raise AssertionError("LDS loads left outstanding at the end of the stream")
+    # nothing in flight at the exit: the compiler may read or overwrite any register right after
+    for r, (wi, wk) in last_w.items():
+        if wk == "mfma" and p - (pos[wi] + st.ins[wi][4]) < MFMA_VALU_RAW:
+            raise AssertionError(f"v{r}: MFMA {wi} may still be writing it when the stream ends")
+    for r, lst in last_r.items():
+        for (ri, role) in lst:
+            if p - (pos[ri] + st.ins[ri][4]) < (SRCC_WAR if role == "C" else SRCAB_WAR):
+                raise AssertionError(f"v{r}: MFMA {ri} may still be reading it when the stream ends")
+
+
+def emit(st):
+    out = []
+    for text, kind, *_ in st.ins:
+        out.append(f'    "{text}\\n"')
+    return "\n".join(out)
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "..", "cudaneuralrender_amd", "csrc", "nr_mlp16_asm.h")
+    parts = [
+        "// nr_mlp16_asm.h -- GENERATED by tools/gen_mlp_asm.py (do not edit; rerun the script).",
+        "// The 16-bit MLP's input layer + 7 hidden layers + the final layer's operand conversion for",
+        "// four 32-point tiles as one software-pipelined stream (see the script's docstring).",
+        "// Registers: accumulators v0-v63 (tile t: v[16t:16t+15]), B operands v64-v95 (tile t, k-step s:",
+        "// v[64+8t+4s:+3]; in: the input layer's B operands in k-step 0's slot; out: the ReLU'd final",
+        "// operands), A operands v96-v111 and biases v112-v143 (two buffers each); %[va] = LDS byte",
+        "// address of the A operands + 16 lane, %[vb] = of the biases + 64 (lane >> 5).",
+        "#pragma once",
+        "",
+    ]
+    for name, prec, clamp in (("NR_HID7_BF16_CLAMP", "bf16", True), ("NR_HID7_BF16_MAX", "bf16", False),
+                              ("NR_HID7_F16_MAX", "fp16", False)):
+        st = build(prec, clamp)
+        nm = sum(1 for x in st.ins if x[1] == "mfma")
+        nv = sum(1 for x in st.ins if x[1] == "valu")
+        parts.append(f"// {prec}, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, {nm} MFMA, {nv} VALU")
+        parts.append(f"#define {name} \\")
+        parts.append(emit(st).replace("\n", " \\\n") + "")
+        parts.append("")
+    text = "\n".join(parts) + "\n"
+    if len(sys.argv) > 1 and sys.argv[1] == "--check":
+        with open(path) as f:
+            if f.read() != text:
+                sys.exit("nr_mlp16_asm.h is stale: rerun tools/gen_mlp_asm.py")
+        return
+    with open(path, "w") as f:
+        f.write(text)
+    print(f"wrote {os.path.normpath(path)}")
+
+
+if __name__ == "__main__":
+    main()

@@ -25,3 +25,17 @@ for part, name in [(0, "full"), (1, "no final layer")]:
         cyc = float(Y[0].item())
         print(f"{name:18s} tiles {nt}: {cyc:.0f} cycles per MLP ({cyc / nt:.0f} per tile; "
               f"MFMA issue floor {114 * 32 * nt})", flush=True)
+
+# the 16-bit MLP on 128 points (k_mlp16's form): the whole evaluation with the pipelined stream,
+# with the builtin form (debug bit 11), and the stream alone
+for prec in ("bf16", "fp16"):
+    r.set_precision(prec)
+    X2 = torch.from_numpy(np.random.default_rng(0).uniform(-1, 1, (130, 3)).astype(np.float32)).cuda()
+    for flags, name in [(64, "whole, stream"), (64 | 2048, "whole, builtin"), (64 | 128, "stream alone")]:
+        r.set_debug(flags)
+        for _ in range(2):
+            r.mlp_forward_device(X2.data_ptr(), Y.data_ptr(), 2000)
+        torch.cuda.synchronize()
+        cyc = float(Y[0].item())
+        print(f"{prec} 128 points {name:16s}: {cyc:.0f} cycles (60 MFMA issue floor {60 * 32})", flush=True)
+r.set_debug(0)
