@@ -152,6 +152,33 @@ def random_poses(n=8):
     return [(float(rng.uniform(-30, 30)), float(rng.uniform(0, 360))) for _ in range(n)]
 
 
+class RankFailed(RuntimeError):
+    """Another rank's render of this batch raised."""
+
+
+def checked_step(dist, world, device, fn):
+    """Runs fn() -- this rank's render of a batch -- and then, before the batch's gather, lets
+    every rank learn whether any rank's fn raised: one all-reduce (MAX) of a status int.  The
+    failing rank re-raises its own error and the others raise RankFailed, so every rank exits
+    within seconds instead of blocking in the gather until the collective times out (SURVEY.md
+    section 5: a per-rank status all-reduce before the gather)."""
+    err = None
+    try:
+        fn()
+    except Exception as e:  # noqa: BLE001 -- re-raised below, after the status exchange
+        err = e
+    failed = 1 if err is not None else 0
+    if world > 1:
+        import torch
+        t = torch.tensor([failed], dtype=torch.int32, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        failed = int(t.item())
+    if err is not None:
+        raise err
+    if failed:
+        raise RankFailed("another rank failed to render its shard of this batch")
+
+
 def self_launch(a):
     """--gpus N > 1 without a launcher: run this script under torch.distributed.run, one
     rank per GPU, as a child process (nothing here has touched a GPU), and return its status."""
@@ -234,20 +261,24 @@ def main():
         if n == 0:
             return
         with torch.cuda.stream(stream):
-            st = r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size,
-                                       [cams[i % len(cams)] for i in range(n)], a.max_steps, BAND, nsh, sh,
-                                       with_stats=True)
-            counted["ray_steps"] += st["ray_steps"]
-            counted["shade_evals"] += st["shade_evals"]
+            def render():
+                st = r.render_batch_device([shards[i].data_ptr() for i in range(n)], size, size,
+                                           [cams[i % len(cams)] for i in range(n)], a.max_steps, BAND, nsh, sh,
+                                           with_stats=True)
+                counted["ray_steps"] += st["ray_steps"]
+                counted["shade_evals"] += st["shade_evals"]
+            checked_step(dist, world, "cuda", render)
             collect(0, n)
 
     def run_single(n):
         with torch.cuda.stream(stream):
             for i in range(n):
-                st = r.render_shard_device(shards[i].data_ptr(), size, size, BAND, nsh, sh, a.max_steps,
-                                           with_stats=True)
-                counted["ray_steps"] += st["ray_steps"]
-                counted["shade_evals"] += st["shade_evals"]
+                def render():
+                    st = r.render_shard_device(shards[i].data_ptr(), size, size, BAND, nsh, sh, a.max_steps,
+                                               with_stats=True)
+                    counted["ray_steps"] += st["ray_steps"]
+                    counted["shade_evals"] += st["shade_evals"]
+                checked_step(dist, world, "cuda", render)
                 collect(i, 1)
 
     def timed(fn, profile):

@@ -81,3 +81,65 @@ def test_gloo_gather_assemble(tmp_path, world, band, nframes, H):
     frames, fulls = np.load(out)
     assert np.array_equal(frames, fulls)
     assert (fulls != 0).sum() > 0
+
+
+def _fail_worker(rank, world, port, bad, result_dir):
+    """bench.py's per-batch step on gloo: rank `bad` raises inside its render; every rank then
+    reaches the gather only if the status all-reduce says every rank rendered."""
+    import sys
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    buf = torch.full((16,), rank, dtype=torch.int64)
+    batch = [0]
+
+    def render():
+        batch[0] += 1
+        if rank == bad and batch[0] == 2:
+            raise RuntimeError("nr_render_batch failed (injected)")
+        buf.add_(1)
+
+    t0 = time.time()
+    outcome = "gathered"
+    try:
+        for _ in range(3):      # three batches: the failure comes in the second
+            bench.checked_step(dist, world, "cpu", render)
+            gl = [torch.zeros(16, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+            dist.gather(buf, gl, dst=0)
+    except bench.RankFailed:
+        outcome = "RankFailed"
+    except RuntimeError as e:
+        outcome = "own error" if "injected" in str(e) else f"other: {e}"
+    with open(os.path.join(result_dir, f"rank{rank}"), "w") as f:
+        f.write(f"{outcome} {time.time() - t0:.2f}")
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (2, 0), (3, 2)])
+def test_failed_rank_fails_fast(tmp_path, world, bad):
+    """a rank whose render raises must not leave the others blocked in the gather.
+    With bench.checked_step before every gather, the failing rank re-raises its error and every
+    other rank raises RankFailed, all within seconds (the gloo default timeout is 30 minutes)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, bad, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a rank is still blocked"
+    res = {r: open(tmp_path / f"rank{r}").read().split() for r in range(world)}
+    for r in range(world):
+        want = "own" if r == bad else "RankFailed"
+        assert res[r][0] == want, res
+        assert float(res[r][-1]) < 60, res
