@@ -23,7 +23,7 @@ EXPORTS = [
     "nr_create", "nr_destroy", "nr_last_error", "nr_abi_version", "nr_set_stream", "nr_synchronize",
     "nr_load_h5", "nr_load_mlp", "nr_mlp_info", "nr_set_precision", "nr_set_view", "nr_set_static",
     "nr_set_scene", "nr_set_matcap", "nr_render", "nr_render_shard", "nr_render_batch", "nr_shard_rows",
-    "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_h5_read_keras",
+    "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_camera_ex", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
     "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
@@ -116,6 +116,7 @@ def lib():
         "nr_mlp_forward": (I, [P, P, P, L64, I]),
         "nr_layer_forward": (I, [P, I, P, P, L64, I]),
         "nr_camera": (I, [F, F, F, F, F, FP, FP]),
+        "nr_camera_ex": (I, [F, F, F, F, F, I, FP, FP]),
         "nr_h5_read_keras": (I, [ctypes.c_char_p, I, IP, IP, FP, ctypes.c_size_t]),
         "nr_h5_open": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),
         "nr_h5_close": (None, [P]),

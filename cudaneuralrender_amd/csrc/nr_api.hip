@@ -1419,8 +1419,14 @@ int nr_dense_forward(nr_ctx *c, const float *W, const float *b, int in, int out,
 }
 
 int nr_camera(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {
+    return nr_camera_ex(rx, ry, zoom, tx, ty, NR_CAMERA_F64, inv_view, normal);
+}
+
+int nr_camera_ex(float rx, float ry, float zoom, float tx, float ty, int mode, float inv_view[12], float normal[16]) {
     if (!inv_view || !normal) return set_err(nullptr, NR_E_INVALID, "nr_camera: NULL output");
-    camera_matrices(rx, ry, zoom, tx, ty, inv_view, normal);
+    if (mode == NR_CAMERA_F64) camera_matrices(rx, ry, zoom, tx, ty, inv_view, normal);
+    else if (mode == NR_CAMERA_EIGEN) camera_matrices_eigen(rx, ry, zoom, tx, ty, inv_view, normal);
+    else return set_err(nullptr, NR_E_INVALID, "nr_camera_ex: unknown mode %d", mode);
     return NR_OK;
 }
 

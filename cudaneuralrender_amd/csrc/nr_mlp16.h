@@ -900,18 +900,8 @@ __device__ __forceinline__ float mlp32_x3_nt(const uint16_t *__restrict__ lp, co
     return (z0 + z1) + F[32];
 }
 
-// wave-uniform: every lane's inputs are within the fp32x3 pack's bounds (NaN is not)
-__device__ __forceinline__ bool inputs_in_bound_x3(float x, float y, float z, float f) {
-    const bool ok = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
-                    __builtin_fabsf(z) <= X3_INPUT_BOUND && __builtin_fabsf(f) <= X3_FRAME_BOUND;
-    return __ballot(!ok) == 0;
-}
-
-// ok (wave-uniform): the fp32x3 pack exists (M.lp_clamp) and every input of the call is within
-// its bounds; otherwise the fp32 MLP (bit-exact, from the fp32 pack) evaluates the wave
-__device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, const uint16_t *lp, const float *fl,
-                                          float fr, float x, float y, float z, uint32_t tmask, bool ok) {
-    if (!ok) return mlp16_fp32(M, s32, fr, x, y, z, tmask);
+__device__ __forceinline__ float mlp16_x3_split(const MlpArgs &M, const uint16_t *lp, const float *fl, float fr, float x,
+                                                float y, float z, uint32_t tmask) {
     if (M.nh == 7) {
         if (tmask & 0xcu) return mlp32_x3_nt<2, 7>(lp, fl, M.in0, M.nh, fr, x, y, z);
         return mlp32_x3_nt<1, 7>(lp, fl, M.in0, M.nh, fr, x, y, z);
@@ -920,14 +910,32 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return mlp32_x3_nt<1, 0>(lp, fl, M.in0, M.nh, fr, x, y, z);
 }
 
+// fp32x3 per point: a point whose inputs are within the pack's bounds gets the split, any other
+// point the fp32 MLP (bit-exact, from the fp32 pack) -- whatever else its wave holds, so a point's
+// value never depends on its batch or chunk.  A wave of in-bound points runs the split
+// alone, a wave of out-of-bound points the fp32 MLP alone, a mixed wave both (each point's column
+// of the products is its own: the other lanes' inputs cannot reach it).  ok = M.lp_clamp: the pack
+// exists (otherwise every point takes the fp32 MLP).
+__device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, const uint16_t *lp, const float *fl,
+                                          float fr, float x, float y, float z, uint32_t tmask, bool ok) {
+    if (!ok) return mlp16_fp32(M, s32, fr, x, y, z, tmask);
+    const bool in = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
+                    __builtin_fabsf(z) <= X3_INPUT_BOUND && __builtin_fabsf(fr) <= X3_FRAME_BOUND;
+    const uint64_t out = __ballot(!in), live = __ballot(in);
+    if (out == 0) return mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+    const float v32 = mlp16_fp32(M, s32, fr, x, y, z, tmask);
+    if (live == 0) return v32;
+    const float v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+    return in ? v3 : v32;
+}
+
 // cl: see mlp16_lowp (ignored in fp32); fp32x3: the pack is valid (M.lp_clamp), the inputs are
 // checked here
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
     if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
-    if (prec == NR_PRECISION_FP32X3)
-        return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0 && inputs_in_bound_x3(x, y, z, fr));
+    if (prec == NR_PRECISION_FP32X3) return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0);
     return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }
 

@@ -445,4 +445,67 @@ void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float i
     normal[15] = 1.0f;
 }
 
+// updateViewMatrices (main.cpp:207-222) in float, restating the scalar (non-vectorised) code
+// paths of Eigen 3.3 that its expression takes (Eigen is not in this image: parity unpinned):
+//   * the angles: -viewRotation.x * M_PI / 180 in double, rounded to float by AngleAxisf;
+//   * AngleAxisf * AngleAxisf is a Quaternionf product (AngleAxis.h operator*): each factor
+//     is (cos(a/2), sin(a/2) axis) (Quaternion.h operator=(AngleAxis)), the product the
+//     generic quat_product (with one axis along x and the other along y, every term but one
+//     of each component is a product with zero, so its rounding is that of a single product:
+//     the SSE quat_product gives the same values);
+//   * Matrix3f m = q: QuaternionBase::toRotationMatrix (tx = 2x, twx = tx w, ...);
+//   * Affine3f::Identity().rotate(m): the linear part is I * m = m;
+//   * .translate(v), v = -viewTranslation: translation = 0 + L v, each row a 3-term redux
+//     in Eigen's unrolled order x0 + (x1 + x2);
+//   * normalMatrix = modelView.matrix().inverse(): the generic 4x4 cofactor inverse
+//     (InverseImpl.h compute_inverse_size4: cofactor_4x4 of general_det3_helper terms, then
+//     division by det = (c0 + c1) + (c2 + c3)).  An SSE build of Eigen inverts 4x4 floats with
+//     a different (Intel) sequence, so the last bits of the normal matrix are the part of this
+//     restatement least likely to match a given reference build.
+void camera_matrices_eigen(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]) {
+    const float ax = (float)((double)(-rx) * 3.14159265358979323846 / 180.0);
+    const float ay = (float)((double)(-ry) * 3.14159265358979323846 / 180.0);
+    // quaternions (w, x, y, z) of the two axis-angle rotations
+    const float hx = 0.5f * ax, hy = 0.5f * ay;
+    const float w1 = std::cos(hx), x1 = std::sin(hx) * 1.0f;  // axis UnitX
+    const float w2 = std::cos(hy), y2 = std::sin(hy) * 1.0f;  // axis UnitY
+    // generic quat_product: a = (w1, x1, 0, 0), b = (w2, 0, y2, 0), evaluated term by term
+    const float z0 = 0.0f;
+    const float qw = w1 * w2 - x1 * z0 - z0 * y2 - z0 * z0;
+    const float qx = w1 * z0 + x1 * w2 + z0 * z0 - z0 * y2;
+    const float qy = w1 * y2 + z0 * w2 + z0 * z0 - x1 * z0;
+    const float qz = w1 * z0 + z0 * z0 + x1 * y2 - z0 * z0;
+    // toRotationMatrix
+    const float txq = 2.0f * qx, tyq = 2.0f * qy, tzq = 2.0f * qz;
+    const float twx = txq * qw, twy = tyq * qw, twz = tzq * qw;
+    const float txx = txq * qx, txy = tyq * qx, txz = tzq * qx;
+    const float tyy = tyq * qy, tyz = tzq * qy, tzz = tzq * qz;
+    float L[3][3];
+    L[0][0] = 1.0f - (tyy + tzz); L[0][1] = txy - twz; L[0][2] = txz + twy;
+    L[1][0] = txy + twz; L[1][1] = 1.0f - (txx + tzz); L[1][2] = tyz - twx;
+    L[2][0] = txz - twy; L[2][1] = tyz + twx; L[2][2] = 1.0f - (txx + tyy);
+    // translate(-viewTranslation), viewTranslation = (tx, ty, -zoom)
+    const float v[3] = {-tx, -ty, -(-zoom)};
+    float T[3];
+    for (int i = 0; i < 3; ++i) T[i] = 0.0f + (L[i][0] * v[0] + (L[i][1] * v[1] + L[i][2] * v[2]));
+    float M[4][4] = {{L[0][0], L[0][1], L[0][2], T[0]}, {L[1][0], L[1][1], L[1][2], T[1]},
+                     {L[2][0], L[2][1], L[2][2], T[2]}, {0.0f, 0.0f, 0.0f, 1.0f}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 4; ++j) inv_view[4 * i + j] = M[i][j];
+    auto det3 = [&](int i1, int i2, int i3, int j1, int j2, int j3) -> float {
+        return M[i1][j1] * (M[i2][j2] * M[i3][j3] - M[i2][j3] * M[i3][j2]);
+    };
+    auto cof = [&](int i, int j) -> float {
+        const int i1 = (i + 1) % 4, i2 = (i + 2) % 4, i3 = (i + 3) % 4;
+        const int j1 = (j + 1) % 4, j2 = (j + 2) % 4, j3 = (j + 3) % 4;
+        return det3(i1, i2, i3, j1, j2, j3) + det3(i2, i3, i1, j1, j2, j3) + det3(i3, i1, i2, j1, j2, j3);
+    };
+    float R[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) R[j][i] = ((i + j) & 1) ? -cof(i, j) : cof(i, j);
+    const float det = (M[0][0] * R[0][0] + M[1][0] * R[0][1]) + (M[2][0] * R[0][2] + M[3][0] * R[0][3]);
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) normal[4 * i + j] = R[i][j] / det;
+}
+
 }  // namespace nr

@@ -113,6 +113,12 @@ namespace nr {
 typedef __attribute__((address_space(1))) uint32_t *gptr_u32;
 
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
+// the A/B knobs' bounds: a shading pass leaves at most SHR - 1 stashed rays, and one
+// iteration adds at most 64; the generated-ray ring is indexed with & (RB - 1)
+static_assert(16 - 1 + 64 <= STASH && NR_SHADE_RAYS_LOWP - 1 + 64 <= STASH && NR_SHADE_RAYS_LOWP >= 1,
+              "NR_SHADE_RAYS_LOWP overflows the per-wave LDS stash");
+static_assert((NR_RING_LOWP & (NR_RING_LOWP - 1)) == 0 && NR_RING_LOWP >= 16 && NR_RING_LOWP <= 64,
+              "NR_RING_LOWP must be a power of two in [16, 64]");
 
 
 // Image row of local row lr of the shard (rows are dealt in bands of A.band).
@@ -693,6 +699,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 #ifndef NR_MLP16_PRIO
 #define NR_MLP16_PRIO 0
 #endif
+// diagnostic build (tools/mlp_stamps.py): per-wave cycle stamps of the 16-bit k_mlp16 loop in Y
+#ifndef NR_MLP16_STAMPS
+#define NR_MLP16_STAMPS 0
+#endif
 // waves per SIMD k_mlp16's registers target (<= 96 VGPRs at 5)
 #ifndef NR_MLP16_WPS
 #define NR_MLP16_WPS 5
@@ -778,6 +788,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             store((uint32_t)(base + 64 + lane), v[1]);
         };
         const int nfull = n & ~127;
+#if NR_MLP16_STAMPS
+        unsigned long long st_mlp = 0;
+        uint32_t st_n = 0;
+#endif
         float nx[2], ny[2], nz[2], nf[2];
         int base = wave * 128;
         load((uint32_t)(base + lane), nx[0], ny[0], nz[0], nf[0]);
@@ -794,6 +808,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             load((uint32_t)(base + stride2 + lane), nx[0], ny[0], nz[0], nf[0]);
             load((uint32_t)(base + stride2 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
             float v[2];
+#if NR_MLP16_STAMPS
+            const unsigned long long ta = __builtin_amdgcn_s_memtime();
+#endif
             constexpr float XB = LP_INPUT_BOUND, FB = LP_INPUT_BOUND;
             const bool ok = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
                             __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
@@ -802,13 +819,30 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                 mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
             else
                 mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+#if NR_MLP16_STAMPS
+            st_mlp += __builtin_amdgcn_s_memtime() - ta;
+            ++st_n;
+#endif
             store((uint32_t)(base + lane), v[0]);
             store((uint32_t)(base + 64 + lane), v[1]);
         };
+#if NR_MLP16_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
         if (base < nfull) {
             body();
             for (base += stride2; base < nfull; base += stride2) body();
         }
+#if NR_MLP16_STAMPS
+        // diagnostic build: per wave {cycles in the loop, of them in the MLP calls, chunks} in Y
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        if (lane == 0) {
+            Y[4 * wave] = (float)(t1 - t0);
+            Y[4 * wave + 1] = (float)st_mlp;
+            Y[4 * wave + 2] = (float)st_n;
+        }
+        return;
+#endif
         // the ragged last chunk (1-127 points): the wave the grid-stride order gives it
         if (nfull < n && (nfull >> 7) % waves == wave) {
             float x[2], y[2], z[2], f[2];
@@ -880,7 +914,9 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         const int m = (int)std::min(SEG, n - p0);
         const float *x = X + p0 * M.in0;
         float *y = Y + p0;
-        const int g = (int)std::min<long>(grid, ((long)m + 255) / 256);
+        // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane)
+        const long per_wg = (prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16) ? 512 : 256;
+        const int g = (int)std::min<long>(grid, ((long)m + per_wg - 1) / per_wg);
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
         const bool four = M.in0 == 4;
         if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);

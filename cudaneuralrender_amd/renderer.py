@@ -19,14 +19,19 @@ def _fptr(a):
     return a.ctypes.data_as(_FP)
 
 
-def camera(rx=0.0, ry=0.0, zoom=2.0, tx=0.0, ty=0.0):
+CAMERA_MODES = {"f64": 0, "eigen": 1}
+
+
+def camera(rx=0.0, ry=0.0, zoom=2.0, tx=0.0, ty=0.0, mode="f64"):
     """updateViewMatrices (main.cpp:207-222): returns (inv_view[12], normal[16]) float32.
 
     ``zoom`` is the value of the reference's ``-z`` flag (default 2): the eye sits at
-    R * (tx, ty, zoom)... i.e. viewTranslation = (tx, ty, -zoom)."""
+    R * (tx, ty, zoom)... i.e. viewTranslation = (tx, ty, -zoom).  ``mode`` "f64": double
+    arithmetic rounded once (nr_camera); "eigen": the reference's float Eigen expression restated
+    (nr_camera_ex NR_CAMERA_EIGEN)."""
     iv = np.zeros(12, np.float32)
     nm = np.zeros(16, np.float32)
-    check(lib().nr_camera(rx, ry, zoom, tx, ty, _fptr(iv), _fptr(nm)))
+    check(lib().nr_camera_ex(rx, ry, zoom, tx, ty, CAMERA_MODES[mode], _fptr(iv), _fptr(nm)))
     return iv, nm
 
 

@@ -261,6 +261,15 @@ int nr_set_poll_interval(nr_ctx *ctx, int every);
  * translate(-(tx, ty, -zoom)); inv_view = rows 0..2 of M, normal = M^-1. */
 int nr_camera(float rx_deg, float ry_deg, float zoom, float tx, float ty,
               float inv_view[12], float normal[16]);
+/* The same with a choice of arithmetic.  NR_CAMERA_F64 (nr_camera's): the rotation and its
+ * exact transpose-inverse in double, rounded once to float.  NR_CAMERA_EIGEN: main.cpp's float
+ * Eigen expression restated step by step -- AngleAxisf * AngleAxisf as a quaternion product,
+ * toRotationMatrix, Affine3f rotate/translate, Matrix4f::inverse by cofactors (Eigen 3.3's scalar
+ * paths; Eigen is not available to pin it, and an SSE build inverts 4x4 floats differently). */
+#define NR_CAMERA_F64 0
+#define NR_CAMERA_EIGEN 1
+int nr_camera_ex(float rx_deg, float ry_deg, float zoom, float tx, float ty, int mode,
+                 float inv_view[12], float normal[16]);
 /* Minimal HDF5 (superblock v0, symbol-table groups, contiguous datasets) Keras
  * reader.  Call with kernels/biases NULL to query sizes. */
 int nr_h5_read_keras(const char *path, int max_layers, int *nlayers, int *dims,

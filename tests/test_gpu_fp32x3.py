@@ -63,25 +63,32 @@ def test_x3_mlp_kat(golden, nets, geom):
     assert not np.array_equal(y, y32)
 
 
-def test_x3_mlp_out_of_bound_waves_fall_back_bitexact(nets):
-    """A 64-point chunk with an input beyond X3_INPUT_BOUND (4) runs the fp32 MLP: bit-exact with
-    the oracle; the other chunks stay on the split."""
+def test_x3_mlp_out_of_bound_points_fall_back_bitexact(nets):
+    """A point with an input beyond X3_INPUT_BOUND (4) runs the fp32 MLP: bit-exact with the
+    oracle.  Every other point stays on the split -- its chunk-mates included, whose values equal
+    those of the same points evaluated with no outlier anywhere (the fallback used to
+    take the whole 64-point wave, so a point's value depended on its chunk)."""
     dims, K, B = nets["plane_1"]
     rng = np.random.default_rng(5)
     X = rng.uniform(-1.2, 1.2, size=(64 * 64, 3)).astype(np.float32)
-    far = [3, 17, 40, 63]
-    for c in far:
-        X[64 * c + 11, 1] = 5.0 if c % 2 else -7.5
+    clean = X.copy()
+    far = [64 * c + 11 for c in (3, 17, 40, 63)] + [64 * 20 + k for k in range(64)]  # + one whole chunk
+    for i in far:
+        X[i, 1] = 5.0 if i % 2 else -7.5
     with nr.Renderer(0) as r:
-        y = r.load_h5(nr.geometry_path("plane_1")).set_precision("fp32x3").mlp_forward(X)[:, 0]
+        r.load_h5(nr.geometry_path("plane_1")).set_precision("fp32x3")
+        y = r.mlp_forward(X)[:, 0]
+        yc = r.mlp_forward(clean)[:, 0]
+        # and the same points shifted by 32: other chunks, other lane halves, same values
+        ys = r.mlp_forward(np.concatenate([clean[:32], X]))[32:, 0]
     y32 = oracle.OracleNet(K, B).forward(X)[:, 0]
-    for c in range(64):
-        sl = slice(64 * c, 64 * c + 64)
-        if c in far:
-            assert np.array_equal(y[sl], y32[sl]), c
-        else:
-            assert not np.array_equal(y[sl], y32[sl]), c
-            assert np.abs(y[sl] - y32[sl]).max() <= 1e-5, c
+    mask = np.zeros(len(X), bool)
+    mask[far] = True
+    assert np.array_equal(y[mask], y32[mask])
+    assert np.array_equal(y[~mask], yc[~mask])
+    assert np.array_equal(ys, y)
+    assert not np.array_equal(y[~mask], y32[~mask])
+    assert np.abs(y[~mask] - y32[~mask]).max() <= 1e-5
 
 
 def test_x3_debug_fallback_renders_fp32_bitexact(nets, chrome):
@@ -178,3 +185,26 @@ def test_x3_pixel_contract(chrome, record, name, geom, size, steps, rows):
     if name == "C2":
         assert x["identical"] >= 0.985 and x["iou"] >= 0.9995, res
         assert abs(st["ray_steps"] - s32["ray_steps"]) <= 1e-3 * s32["ray_steps"], (st, s32)
+
+
+def test_x3_batch_frames_straddling_bound():
+    """A 4-input network (the frame as 4th input): frames beyond X3_FRAME_BOUND (1024) take the
+    fp32 MLP, the others the split -- per point, so a batch holding frames on both sides of the
+    bound gives every frame the pixels of its own single-frame render."""
+    rng = np.random.default_rng(12)
+    dims = [4] + [32] * 8 + [1]
+    K = [rng.normal(0, 0.3, size=(dims[i], dims[i + 1])).astype(np.float32) for i in range(len(dims) - 1)]
+    K[0][3] *= 0.0005
+    B = [rng.normal(0, 0.05, size=dims[i + 1]).astype(np.float32) for i in range(len(dims) - 1)]
+    B[-1][0] = 0.2
+    iv, nm = nr.camera(0, 0, 2)
+    frames = [3, 1500, 1024, 1025, 7]
+    with nr.Renderer(0) as r:
+        r.load_mlp(dims, K, B).set_precision("fp32x3").set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
+        singles = []
+        for f in frames:
+            r.set_view(iv, nm, f)
+            singles.append(r.render(80, 64, 64)[0])
+        imgs, _ = r.render_batch(80, 64, [(iv, nm, f) for f in frames], 64)
+    assert all(np.array_equal(a, b) for a, b in zip(imgs, singles))
+    assert any((s != 0).any() for s in singles)

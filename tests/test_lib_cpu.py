@@ -98,7 +98,8 @@ def test_ppm_writer(tmp_path):
 
 
 def camera_ref(rx, ry, zoom):
-    """numpy restatement of updateViewMatrices (main.cpp:207-222)."""
+    """numpy f64 restatement of updateViewMatrices (main.cpp:207-222) on the float arguments."""
+    rx, ry, zoom = float(np.float32(rx)), float(np.float32(ry)), float(np.float32(zoom))
     ax, ay = -np.radians(rx), -np.radians(ry)
     Rx = np.array([[1, 0, 0], [0, np.cos(ax), -np.sin(ax)], [0, np.sin(ax), np.cos(ax)]])
     Ry = np.array([[np.cos(ay), 0, np.sin(ay)], [0, 1, 0], [-np.sin(ay), 0, np.cos(ay)]])
@@ -109,14 +110,98 @@ def camera_ref(rx, ry, zoom):
     return M[:3].reshape(-1), np.linalg.inv(M).reshape(-1)
 
 
-@pytest.mark.parametrize("rx,ry,zoom", [(0, 0, 2), (-18.3, 150.7, 2.25), (45, -30, 3.0), (-79, 229, 3.05)])
+CAMS = [(0, 0, 2), (-18.3, 150.7, 2.25), (45, -30, 3.0), (-79, 229, 3.05), (90, 180, 2.0), (-18.8021, 149.7984, 2.2702),
+        (0, 37.0, 4.0), (12.5, 0, 1.5)]
+
+
+def _ulps(a, b):
+    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
+    return np.abs(a.view(np.int32).astype(np.int64) - b.view(np.int32).astype(np.int64))
+
+
+@pytest.mark.parametrize("rx,ry,zoom", CAMS)
 def test_camera(rx, ry, zoom):
+    """NR_CAMERA_F64 (nr_camera): the f64 rotation and its exact transpose-inverse, rounded once:
+    within 1 ulp of numpy's f64 evaluation rounded to f32 (where both are not ~0), and M^-1 M = I."""
     iv, nm = nr.camera(rx, ry, zoom)
     riv, rnm = camera_ref(rx, ry, zoom)
-    assert np.allclose(iv, riv, atol=1e-6) and np.allclose(nm, rnm, atol=1e-6)
+    for got, ref in ((iv, riv), (nm, rnm)):
+        big = np.abs(ref) > 1e-6
+        assert (_ulps(got[big], ref[big].astype(np.float32)) <= 1).all(), (got, ref)
+        assert np.abs(got[~big] - ref[~big]).max(initial=0) <= 1e-6
+    M = np.eye(4)
+    M[:3] = iv.reshape(3, 4)
+    assert np.abs(M @ nm.reshape(4, 4).astype(np.float64) - np.eye(4)).max() < 1e-6
     if rx == 0 and ry == 0:
         # default camera: eye at (0, 0, 2)
-        assert list(iv) == [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 2]
+        assert list(iv) == [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, zoom]
+
+
+def camera_eigen_np(rx, ry, zoom, tx=0.0, ty=0.0):
+    """numpy float32 restatement of main.cpp:207-222 through Eigen 3.3's scalar paths (the
+    independent check of nr_pack.cpp camera_matrices_eigen): AngleAxisf * AngleAxisf as a
+    quaternion product, toRotationMatrix, rotate, translate (3-term redux x0 + (x1 + x2)),
+    cofactor 4x4 inverse with det = (c0 + c1) + (c2 + c3)."""
+    import math
+    f = np.float32
+    ax = f(float(-f(rx)) * math.pi / 180.0)
+    ay = f(float(-f(ry)) * math.pi / 180.0)
+    hx, hy = f(0.5) * ax, f(0.5) * ay
+    w1, x1 = f(math.cos(hx)), f(math.sin(hx))
+    w2, y2 = f(math.cos(hy)), f(math.sin(hy))
+    z = f(0)
+    qw = w1 * w2 - x1 * z - z * y2 - z * z
+    qx = w1 * z + x1 * w2 + z * z - z * y2
+    qy = w1 * y2 + z * w2 + z * z - x1 * z
+    qz = w1 * z + z * z + x1 * y2 - z * z
+    tx_, ty_, tz_ = f(2) * qx, f(2) * qy, f(2) * qz
+    twx, twy, twz = tx_ * qw, ty_ * qw, tz_ * qw
+    txx, txy, txz = tx_ * qx, ty_ * qx, tz_ * qx
+    tyy, tyz, tzz = ty_ * qy, tz_ * qy, tz_ * qz
+    L = [[f(1) - (tyy + tzz), txy - twz, txz + twy],
+         [txy + twz, f(1) - (txx + tzz), tyz - twx],
+         [txz - twy, tyz + twx, f(1) - (txx + tyy)]]
+    v = [-f(tx), -f(ty), -(-f(zoom))]
+    T = [f(0) + (L[i][0] * v[0] + (L[i][1] * v[1] + L[i][2] * v[2])) for i in range(3)]
+    M = [[L[0][0], L[0][1], L[0][2], T[0]], [L[1][0], L[1][1], L[1][2], T[1]],
+         [L[2][0], L[2][1], L[2][2], T[2]], [z, z, z, f(1)]]
+
+    def det3(i1, i2, i3, j1, j2, j3):
+        return M[i1][j1] * (M[i2][j2] * M[i3][j3] - M[i2][j3] * M[i3][j2])
+
+    def cof(i, j):
+        i1, i2, i3, j1, j2, j3 = (i + 1) % 4, (i + 2) % 4, (i + 3) % 4, (j + 1) % 4, (j + 2) % 4, (j + 3) % 4
+        return det3(i1, i2, i3, j1, j2, j3) + det3(i2, i3, i1, j1, j2, j3) + det3(i3, i1, i2, j1, j2, j3)
+
+    R = [[z] * 4 for _ in range(4)]
+    for i in range(4):
+        for j in range(4):
+            R[j][i] = -cof(i, j) if (i + j) % 2 else cof(i, j)
+    det = (M[0][0] * R[0][0] + M[1][0] * R[0][1]) + (M[2][0] * R[0][2] + M[3][0] * R[0][3])
+    iv = np.array([M[i][j] for i in range(3) for j in range(4)], np.float32)
+    nm = np.array([R[i][j] / det for i in range(4) for j in range(4)], np.float32)
+    return iv, nm
+
+
+@pytest.mark.parametrize("rx,ry,zoom", CAMS)
+def test_camera_eigen_float(rx, ry, zoom):
+    """NR_CAMERA_EIGEN restates the reference's float Eigen camera.  Parity with
+    Eigen itself is unpinned (Eigen is not in this image); checked here: bit-equal to an
+    independent numpy float32 restatement of the same Eigen 3.3 code paths, a few ulps from the
+    f64 form, a rotation (R R^T = I to float precision), and M^-1 M = I."""
+    iv, nm = nr.camera(rx, ry, zoom, mode="eigen")
+    riv, rnm = camera_eigen_np(rx, ry, zoom)
+    assert np.array_equal(iv, riv), (iv, riv)
+    assert np.array_equal(nm, rnm), (nm, rnm)
+    fiv, fnm = nr.camera(rx, ry, zoom)
+    assert np.abs(iv - fiv).max() <= 4e-6 * max(1.0, zoom) and np.abs(nm - fnm).max() <= 4e-6 * max(1.0, zoom)
+    R = iv.reshape(3, 4)[:, :3].astype(np.float64)
+    assert np.abs(R @ R.T - np.eye(3)).max() < 1e-6
+    M = np.eye(4)
+    M[:3] = iv.reshape(3, 4)
+    assert np.abs(M @ nm.reshape(4, 4).astype(np.float64) - np.eye(4)).max() < 1e-5
+    if rx == 0 and ry == 0:
+        assert list(iv) == [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, zoom]
 
 
 @pytest.mark.parametrize("H,band,n", [(1024, 8, 8), (1024, 8, 3), (83, 5, 3), (7, 8, 2), (1, 1, 4), (100, 1, 7)])

@@ -32,6 +32,8 @@ static Image matcap;
 
 struct dim3_ { unsigned x, y, z; };
 
+static int cameraMode = NR_CAMERA_EIGEN;  // updateViewMatrices' arithmetic (--camera)
+
 static char *getCmdOption(char **begin, char **end, const std::string &option) {
     char **itr = std::find(begin, end, option);
     if (itr != end && ++itr != end) return *itr;
@@ -53,7 +55,8 @@ static void usage() {
                  "\t--single render one frame and save it\n"
                  "\t--spin render 360 frames rotating about y\n"
                  "\t--animation 4-input networks (frame number as 4th input)\n"
-                 "\t--max-steps N (default 6000)  --precision fp32|bf16|fp16|fp32x3  --scene v1|tanh  --ppm\n";
+                 "\t--max-steps N (default 6000)  --precision fp32|bf16|fp16|fp32x3  --scene v1|tanh  --ppm\n"
+                 "\t--camera eigen|f64 (default eigen: main.cpp's float Eigen arithmetic; f64: rounded once)\n";
 }
 
 static void parseCmdOptions(int argc, char **argv) {
@@ -71,6 +74,7 @@ static void parseCmdOptions(int argc, char **argv) {
     doSpin = cmdOptionExists(b, e, "--spin");
     singleImage = cmdOptionExists(b, e, "--single");
     writePPM = cmdOptionExists(b, e, "--ppm");
+    if (getCmdOption(b, e, "--camera")) cameraMode = std::string(getCmdOption(b, e, "--camera")) == "f64" ? NR_CAMERA_F64 : NR_CAMERA_EIGEN;
     if (cmdOptionExists(b, e, "--animation")) numInputs = 4;
     if (getCmdOption(b, e, "--max-steps")) NR_MAX_STEPS = atoi(getCmdOption(b, e, "--max-steps"));
     if (getCmdOption(b, e, "--scene")) NR_SCENE_MODE = std::string(getCmdOption(b, e, "--scene")) == "tanh" ? NR_SCENE_TANH : NR_SCENE_V1;
@@ -93,7 +97,7 @@ static bool generateSingleImage() {
     if (hipMalloc(&d_output, (size_t)width * height * sizeof(unsigned)) != hipSuccess) return false;
     (void)hipMemset(d_output, 0, (size_t)width * height * sizeof(unsigned));
     float invView[12], normal[16];
-    nr_camera(rotX, rotY, zoom, 0.0f, 0.0f, invView, normal);  // updateViewMatrices
+    nr_camera_ex(rotX, rotY, zoom, 0.0f, 0.0f, cameraMode, invView, normal);  // updateViewMatrices
     copyViewMatrices(invView, sizeof invView, normal, sizeof normal, frameNumber);
     (void)hipDeviceSynchronize();
     auto t0 = std::chrono::steady_clock::now();
