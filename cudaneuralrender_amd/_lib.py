@@ -29,6 +29,7 @@ EXPORTS = [
     "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
     "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
     "nr_h5_dims", "nr_h5_read_f32",
+    "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch",
 ]
 
 
@@ -110,6 +111,10 @@ def lib():
         "nr_render": (I, [P, P, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_render_shard": (I, [P, P, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
+        "nr_group_create": (I, [ctypes.POINTER(P), I, ctypes.POINTER(P)]),
+        "nr_group_destroy": (I, [P]),
+        "nr_group_size": (I, [P]),
+        "nr_group_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_shard_rows": (I, [I, I, I, I]),
         "nr_batch_frames_per_launch": (I, [I, I, I, I, I, I, I]),
         "nr_assemble_shards": (I, [P, P, ctypes.c_size_t, P, I, I, I, I, I]),

@@ -1487,3 +1487,9 @@ int nr_ppm_save(const char *path, const uint32_t *rgba, int w, int h) {
 void nr_free(void *p) { free(p); }
 
 }  // extern "C"
+
+// context internals for nr_group.hip (nr_internal.h)
+namespace nr {
+int ctx_device(const nr_ctx *c) { return c->device; }
+void *ctx_stream(nr_ctx *c) { return (void *)cur_stream(c); }
+}  // namespace nr

@@ -103,6 +103,10 @@ bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<floa
                 const std::vector<std::vector<float>> &biases, std::vector<uint16_t> &a_ops, std::vector<float> &fl,
                 int *ok = nullptr);
 
+// ---- context internals for nr_group.hip (nr_api.hip) ----
+int ctx_device(const nr_ctx *c);
+void *ctx_stream(nr_ctx *c);  // the hipStream_t the context's work runs on (creates its own stream if selected)
+
 // ---- camera (nr_pack.cpp; the C ABI's nr_camera) ----
 void camera_matrices(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]);
 void camera_matrices_eigen(float rx, float ry, float zoom, float tx, float ty, float inv_view[12], float normal[16]);

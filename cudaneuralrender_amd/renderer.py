@@ -354,3 +354,54 @@ class Renderer:
 
 __all__ = ["Renderer", "camera", "read_keras_h5", "load_png", "save_png", "save_ppm", "shard_rows",
            "assemble_shards", "NR_COLOR_FACING", "NR_COLOR_MATCAP"]
+
+
+class Group:
+    """nr_group: renderers on distinct GPUs of one process joined by one RCCL communicator.
+    render_batch splits every frame into row-band shards (renderer r renders shard r), checks
+    every shard's status, gathers the shards to the first renderer's GPU in one RCCL call and
+    re-interleaves them there (include/neural_render.h nr_group_render_batch)."""
+
+    def __init__(self, renderers):
+        self._L = lib()
+        self.renderers = list(renderers)
+        arr = (ctypes.c_void_p * len(self.renderers))(*[r._ctx.value for r in self.renderers])
+        self._g = ctypes.c_void_p()
+        check(self._L.nr_group_create(arr, len(self.renderers), ctypes.byref(self._g)))
+
+    def close(self):
+        if self._g:
+            self._L.nr_group_destroy(self._g)
+            self._g = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def size(self):
+        return self._L.nr_group_size(self._g)
+
+    def render_batch(self, W, H, cams, max_steps=6000, band=1, with_stats=True):
+        """Full frames (H, W) on the host for cams = [(inv_view, normal[, frame]), ...]."""
+        outs = [np.zeros((H, W), np.uint32) for _ in cams]
+        fr = Renderer._frames(cams, [o.ctypes.data for o in outs])
+        st = NRStats()
+        check(self._L.nr_group_render_batch(self._g, fr, len(cams), W, H, band, max_steps, NR_HOST,
+                                            ctypes.byref(st) if with_stats else None))
+        return (outs, st.as_dict()) if with_stats else outs
+
+    def render_batch_device(self, out_ptrs, W, H, cams, max_steps=6000, band=1, with_stats=False):
+        """Full frames into device buffers on the first renderer's GPU."""
+        fr = Renderer._frames(cams, list(out_ptrs))
+        st = NRStats()
+        check(self._L.nr_group_render_batch(self._g, fr, len(cams), W, H, band, max_steps, NR_DEVICE,
+                                            ctypes.byref(st) if with_stats else None))
+        return st.as_dict() if with_stats else None

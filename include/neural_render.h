@@ -162,6 +162,24 @@ int nr_batch_frames_per_launch(int W, int H, int band_rows, int nshards, int sha
 int nr_assemble_shards(nr_ctx *ctx, const uint32_t *src, size_t stride_pixels,
                        uint32_t *dst, int W, int H, int band_rows, int nshards, int loc);
 
+/* ---- multi-GPU, one process (main.cpp's render loop over the GPUs of a node) --------------
+ * A group joins contexts on distinct GPUs (each created by nr_create on its device, with the
+ * same network, precision, scene, colouring, matcap and schedule settings) with one RCCL
+ * communicator (ncclCommInitAll).  nr_group_render_batch renders nframes frames across them:
+ * context r renders row-band shard r of every frame (bands of `band` rows dealt round-robin,
+ * the contexts in parallel, one host thread each), every shard's status is checked before any
+ * transfer (a failed shard returns its error and starts no collective), ONE RCCL gather per call
+ * (ncclSend / ncclRecv in one ncclGroupStart / ncclGroupEnd) brings the shards to the first
+ * context's GPU, and one re-interleave launch per frame writes frames[i].out -- device pointers
+ * on the first context's GPU (loc = NR_DEVICE) or host pointers (NR_HOST).  Pixels are
+ * identical to nr_render on one GPU.  stats: summed over the shards (ms_total: the slowest). */
+typedef struct nr_group nr_group;
+int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out);
+int nr_group_destroy(nr_group *group);
+int nr_group_size(const nr_group *group);
+int nr_group_render_batch(nr_group *group, const nr_frame *frames, int nframes, int W, int H, int band,
+                          int max_steps, int loc, nr_stats *stats);
+
 /* Replaces NeuralNetwork::forward(X) (neuralNetwork.cpp:54-63) on a batch:
  * X [n][dims[0]] fp32, Y [n][dims[nlayers]] fp32.  loc = NR_HOST or NR_DEVICE. */
 int nr_mlp_forward(nr_ctx *ctx, const float *X, float *Y, long n, int loc);

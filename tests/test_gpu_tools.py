@@ -81,3 +81,21 @@ def test_renderer_camera_f64(tmp_path):
     ref, _ = oracle.OracleNet(K, B).render(64, 48, iv, nm, color_type=1, matcap=nr.load_png(nr.matcap_path("Chrome")),
                                            max_steps=128)
     assert np.array_equal(png, ref[::-1, ::-1])
+
+
+def test_renderer_gpus_group(tmp_path):
+    """--gpus N (nr_group_render_batch: row-band shards on N GPUs, one RCCL gather): on the
+    one-GPU box N = 1, whose frame (through the RCCL send/recv and the re-interleave) equals the
+    single-GPU render_kernel path's."""
+    base = [os.path.join(BIN, "neuralSDFRenderer"), "-i", nr.geometry_path("car_1"), "-W", "72", "-H", "56",
+            "-rx", "-12", "-ry", "40", "--single", "--max-steps", "128", "-M", nr.matcap_path("Chrome")]
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    p = run(base + ["-o", str(a) + "/"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    p = run(base + ["-o", str(b) + "/", "--gpus", "1"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "NumDevsUsed = 1" in p.stdout
+    ia, ib = nr.load_png(str(a / "car_1.h5.png")), nr.load_png(str(b / "car_1.h5.png"))
+    assert np.array_equal(ia, ib) and (ia != 0).any()

@@ -4,7 +4,9 @@
 // and spin modes (:404-478), output naming (:445-461), PNG with the reference's
 // 180-degree rotation, and the throughput printf (:436-437).  The GLUT interactive
 // viewer (:480-519) needs a display and is not built; extra flags: --max-steps,
-// --precision {fp32,bf16,fp16,fp32x3}, --scene {v1,tanh}, --ppm (also write a .ppm).
+// --precision {fp32,bf16,fp16,fp32x3}, --scene {v1,tanh}, --ppm (also write a .ppm),
+// --camera {eigen,f64}, --gpus N (each frame's row-band shards on N GPUs, one RCCL gather:
+// nr_group_render_batch).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -14,6 +16,7 @@
 #include <cstring>
 #include <iostream>
 #include <string>
+#include <vector>
 
 #include "neural_render.h"
 #include "nr/image.hh"
@@ -33,6 +36,11 @@ static Image matcap;
 struct dim3_ { unsigned x, y, z; };
 
 static int cameraMode = NR_CAMERA_EIGEN;  // updateViewMatrices' arithmetic (--camera)
+// --gpus N: every frame split into row-band shards over GPUs 0..N-1 of this process (one context
+// per GPU, nr_group: one RCCL gather per frame); 0 = the reference's single-GPU render_kernel path
+static int numGpus = 0;
+static std::vector<nr_ctx *> groupCtx;
+static nr_group *group = nullptr;
 
 static char *getCmdOption(char **begin, char **end, const std::string &option) {
     char **itr = std::find(begin, end, option);
@@ -56,7 +64,8 @@ static void usage() {
                  "\t--spin render 360 frames rotating about y\n"
                  "\t--animation 4-input networks (frame number as 4th input)\n"
                  "\t--max-steps N (default 6000)  --precision fp32|bf16|fp16|fp32x3  --scene v1|tanh  --ppm\n"
-                 "\t--camera eigen|f64 (default eigen: main.cpp's float Eigen arithmetic; f64: rounded once)\n";
+                 "\t--camera eigen|f64 (default eigen: main.cpp's float Eigen arithmetic; f64: rounded once)\n"
+                 "\t--gpus N split every frame into row-band shards over N GPUs (one RCCL gather per frame)\n";
 }
 
 static void parseCmdOptions(int argc, char **argv) {
@@ -76,6 +85,7 @@ static void parseCmdOptions(int argc, char **argv) {
     writePPM = cmdOptionExists(b, e, "--ppm");
     if (getCmdOption(b, e, "--camera")) cameraMode = std::string(getCmdOption(b, e, "--camera")) == "f64" ? NR_CAMERA_F64 : NR_CAMERA_EIGEN;
     if (cmdOptionExists(b, e, "--animation")) numInputs = 4;
+    if (getCmdOption(b, e, "--gpus")) numGpus = std::max(0, atoi(getCmdOption(b, e, "--gpus")));
     if (getCmdOption(b, e, "--max-steps")) NR_MAX_STEPS = atoi(getCmdOption(b, e, "--max-steps"));
     if (getCmdOption(b, e, "--scene")) NR_SCENE_MODE = std::string(getCmdOption(b, e, "--scene")) == "tanh" ? NR_SCENE_TANH : NR_SCENE_V1;
     if (getCmdOption(b, e, "--precision")) {
@@ -92,7 +102,50 @@ static int countDigit(unsigned n) {
     return c;
 }
 
+static bool saveFrame(Image &out);
+
+// One context per GPU with the same network and settings, joined into an nr_group.
+static bool groupInit() {
+    for (int d = 0; d < numGpus; ++d) {
+        nr_ctx *c = nullptr;
+        if (nr_create(d, &c) != NR_OK || nr_load_h5(c, neuralGeometryPath.c_str()) != NR_OK ||
+            nr_set_precision(c, NR_PRECISION_MODE) != NR_OK || nr_set_scene(c, NR_SCENE_MODE) != NR_OK ||
+            nr_set_static(c, colorType, numInputs) != NR_OK ||
+            (colorType == NR_COLOR_MATCAP &&
+             nr_set_matcap(c, matcap.hostData.get(), (int)matcap.shape.x, (int)matcap.shape.y) != NR_OK)) {
+            printf("GPU %d: %s\n", d, nr_last_error(c));
+            return false;
+        }
+        groupCtx.push_back(c);
+    }
+    if (nr_group_create(groupCtx.data(), numGpus, &group) != NR_OK) {
+        printf("nr_group_create: %s\n", nr_last_error(nullptr));
+        return false;
+    }
+    return true;
+}
+
 static bool generateSingleImage() {
+    if (numGpus > 0) {  // the frame across numGpus GPUs
+        if (!group && !groupInit()) return false;
+        nr_frame f{};
+        nr_camera_ex(rotX, rotY, zoom, 0.0f, 0.0f, cameraMode, f.inv_view, f.normal);
+        f.frame = frameNumber;
+        Image out(width, height, true);
+        out.allocateMemory();
+        f.out = out.hostData.get();
+        auto t0 = std::chrono::steady_clock::now();
+        if (nr_group_render_batch(group, &f, 1, (int)width, (int)height, 1, NR_MAX_STEPS, NR_HOST, nullptr) != NR_OK) {
+            printf("nr_group_render_batch: %s\n", nr_last_error(nullptr));
+            return false;
+        }
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (saveCount == 0)
+            printf("volumeRender, Throughput = %.4f MTexels/s, Time = %.5f s, Size = %u Texels, NumDevsUsed = %d, "
+                   "Workgroup = %u\n",
+                   (1.0e-6 * width * height) / dt, dt, width * height, numGpus, 256u);
+        return saveFrame(out);
+    }
     unsigned *d_output = nullptr;
     if (hipMalloc(&d_output, (size_t)width * height * sizeof(unsigned)) != hipSuccess) return false;
     (void)hipMemset(d_output, 0, (size_t)width * height * sizeof(unsigned));
@@ -112,6 +165,12 @@ static bool generateSingleImage() {
     Image out(width, height, true);
     out.allocateMemory();
     (void)hipMemcpy(out.hostData.get(), d_output, (size_t)width * height * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_output);
+    return saveFrame(out);
+}
+
+// main.cpp:445-461: the frame's file name and PNG (+ PPM)
+static bool saveFrame(Image &out) {
     std::string ext;
     if (!singleImage) {
         if (countDigit(saveCount) < 2) ext += "00";
@@ -125,7 +184,6 @@ static bool generateSingleImage() {
     bool ok = out.savePNG(renderSavePath + ext);
     if (writePPM) ok = out.savePPM(renderSavePath + ext + ".ppm") && ok;
     ++saveCount;
-    (void)hipFree(d_output);
     return ok;
 }
 
