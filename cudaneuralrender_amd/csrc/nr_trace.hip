@@ -166,6 +166,16 @@ static_assert(sizeof(FrameLds) == 72 && offsetof(FrameLds, zoff) == 48 && offset
 static_assert(offsetof(FrameArgs, zoff) == 112 && offsetof(FrameArgs, out) == 120 && offsetof(FrameArgs, frame_f) == 128,
               "FrameArgs layout (staged word by word in k_trace)");
 
+// The atomic add of lane 0 on pixel-queue shard sh (its counter on a 128-byte line), issued by every
+// lane -- lanes 1-63 at an offset past the counters, dropped by the buffer's range check -- so that no
+// lane-divergent branch surrounds it: around `if (lane == 0) v = atomicAdd(..)` hipcc waited for
+// the return at the branch's join, which made the reservation requested one refill ahead
+// (NR_QUEUE_PREFETCH) a full round trip to memory at every request.  Returns lane 0's old value
+// (read it with readfirstlane where it is needed).
+__device__ __forceinline__ uint32_t queue_add(const __amdgpu_buffer_rsrc_t rq, int lane, int sh, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)v, rq, lane == 0 ? sh * 128 : 0x7fffff00, 0, 0);
+}
+
 // s_setprio takes an immediate
 __device__ __forceinline__ void set_priority(int prio) {
     switch (prio) {
@@ -234,6 +244,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
+    const auto rq = __builtin_amdgcn_make_buffer_rsrc(T.pix_ctr, 0, 128 << T.nq_shift, 0x00020000);  // the shard counters
     const float fr = (float)A.frame;
     const double zoff0 = sphere_zoff(A.frame);
     // frame-dependent values of frame f (single-frame launches: the uniform ones in A)
@@ -321,9 +332,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             while (pool_cnt == 0) {  // nothing reserved: a blocking reservation
                                 const long tot = shard_total(shard);
                                 const uint32_t w = max(want, (uint32_t)QCHUNK);
-                                uint32_t b = 0;
-                                if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, w);
-                                b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);  // lane 0: the whole wave is active
+                                const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)queue_add(rq, lane, shard, w));
                                 if ((long)b < tot) {
                                     pool_base = b;
                                     pool_cnt = (uint32_t)min((long)w, tot - (long)b);
@@ -344,15 +353,13 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                             pool_cnt -= got;
                         }
                         if (!qempty && !pend && pool_cnt < QLOW) {
-                            if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)QCHUNK);
+                            pend_v = queue_add(rq, lane, shard, (uint32_t)QCHUNK);
                             pend = true;
                         }
                     } else {
                         while (true) {
                             const long total = shard_total(shard);
-                            uint32_t b = 0;
-                            if (lane == 0) b = atomicAdd(T.pix_ctr + shard * 32, want);
-                            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+                            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)queue_add(rq, lane, shard, want));
                             if ((long)base < total) {
                                 got = (uint32_t)min((long)want, total - (long)base);
                                 break;
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                 }
                             }
                             if (!qempty && !pend && pool_cnt < QLOW) {
-                                if (lane == 0) pend_v = atomicAdd(T.pix_ctr + shard * 32, (uint32_t)QCHUNK);
+                                pend_v = queue_add(rq, lane, shard, (uint32_t)QCHUNK);
                                 pend = true;
                             }
                         } else {
@@ -703,6 +710,12 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 #ifndef NR_MLP16_STAMPS
 #define NR_MLP16_STAMPS 0
 #endif
+// counters of k_mlp16's chunk queue (a power of two): one word serves ~88 atomics per us
+// (MI355X_MICROARCH.md 'dequeue'), and a 2^24-point bf16 launch takes ~800 chunks per us
+#ifndef NR_MLP16_QSHARDS
+#define NR_MLP16_QSHARDS 16
+#endif
+static_assert((NR_MLP16_QSHARDS & (NR_MLP16_QSHARDS - 1)) == 0 && NR_MLP16_QSHARDS <= 32, "queue shards");
 // waves per SIMD k_mlp16's registers target (<= 96 VGPRs at 5)
 #ifndef NR_MLP16_WPS
 #define NR_MLP16_WPS 5
@@ -764,7 +777,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         // input loads to their use: with the ragged chunk inside it, the merge of its one-store path
         // made hipcc wait for this chunk's stores too (s_waitcnt vmcnt(0) on every chunk, a store's
         // round trip to memory).  The ragged last chunk follows the loop, on the wave whose turn it is.
-        const int stride2 = waves * 128;
         auto run = [&](int base, const float (&x)[2], const float (&y)[2], const float (&z)[2], const float (&f)[2]) {
             const int rem = n - base;
             // the bf16 clamped pack's input bound (NaN is not within it)
@@ -792,22 +804,81 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         unsigned long long st_mlp = 0;
         uint32_t st_n = 0;
 #endif
+        // The whole chunks are dealt by a queue (M.queue: NR_MLP16_QSHARDS counters, one per 128-byte
+        // line, zeroed before the launch) to a persistent grid: shard s holds chunks s, s + Q, s + 2Q,
+        // ... (Q shards); a wave takes one chunk of its shard per atomic and moves to the next shard
+        // once its own is dry.  Dealt this way, a SIMD that runs slower (clock, placement) takes
+        // fewer chunks: with a fixed grid-stride share the last wave of a launch ended 13 % after the
+        // median one (tools/mlp_stamps.py).  The indices run two chunks ahead: the claim for chunk
+        // i + 2 is issued at the top of chunk i and read at its end, so its ~1-2 us round trip hides
+        // under the MLP with no branch in between.  The atomic is a buffer atomic every lane issues,
+        // lanes 1-63 at an offset past the buffer (dropped by the range check): no lane-divergent
+        // branch, whose join would wait for the return at once.
+        // M.queue == nullptr: the fixed grid-stride order (a wave's chunks wave, wave + waves, ...).
+        constexpr int Q = NR_MLP16_QSHARDS;
+        const uint32_t nch = (uint32_t)(nfull >> 7);
+        const auto rq = buffer_of(M.queue, (uint32_t)Q * 128u);
+        const uint32_t qlane = lane == 0 ? 0u : 0x7fffff00u;
+        int sh = wave & (Q - 1), tries = 0, gs = wave;
+        auto claim = [&]() -> int {  // issued, not waited for (lane 0 holds the position)
+            return __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, (int)(qlane + (uint32_t)sh * 128u), 0, 0);
+        };
+        auto shard_n = [&](int s) -> uint32_t {
+            return nch > (uint32_t)s ? (nch - 1u - (uint32_t)s) / (uint32_t)Q + 1u : 0u;
+        };
+        // the chunk of claim result r (lane 0's position in shard sh); past the shard: the next
+        // shards, by blocking claims; -1 when every shard is dry (wave-uniform)
+        auto settle = [&](int r) -> int {
+            uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(r);
+            while (v >= shard_n(sh)) {
+                if (++tries >= Q) return -1;
+                sh = (sh + 1) & (Q - 1);
+                v = (uint32_t)__builtin_amdgcn_readfirstlane(claim());
+            }
+            return (int)(v * (uint32_t)Q + (uint32_t)sh);
+        };
+        auto fixed = [&]() -> int {
+            const int c = gs;
+            gs += waves;
+            return c < (int)nch ? c : -1;
+        };
+        int cur, nxt;
+        if (M.queue) {
+            cur = settle(claim());
+            nxt = cur < 0 ? -1 : settle(claim());
+        } else {
+            cur = fixed();
+            nxt = fixed();
+        }
         float nx[2], ny[2], nz[2], nf[2];
-        int base = wave * 128;
-        load((uint32_t)(base + lane), nx[0], ny[0], nz[0], nf[0]);
-        load((uint32_t)(base + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
-        // One chunk: its inputs (requested one chunk ahead) -> the next chunk's request -> MLP ->
-        // stores.  The first chunk is peeled off the loop, so that the loop is entered with the
-        // memory operations in flight that it is re-entered with (a chunk's two loads, then the
-        // previous chunk's two stores): hipcc merges the entry's and the back edge's wait counts,
-        // and with no stores on the entry path it waited for the previous chunk's stores before
-        // every chunk (a store's round trip to memory per chunk).
+        const int c0 = cur < 0 ? (int)nch : cur;
+        load((uint32_t)(c0 * 128 + lane), nx[0], ny[0], nz[0], nf[0]);
+        load((uint32_t)(c0 * 128 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+        // the first chunk's inputs, waited for here (s_waitcnt vmcnt(0)): the loop is then entered
+        // with nothing in flight, and hipcc's merge of the entry path into the loop's wait counts
+        // adds no wait to the back edge (where the inputs arrive by copies waited for a chunk earlier)
+        __builtin_amdgcn_s_waitcnt(0x0f70);
+        // One chunk: wait for its inputs (requested one chunk earlier) -> every memory operation of
+        // the iteration: the next chunk's input loads, the previous chunk's stores (its outputs were
+        // kept in registers), the claim for the chunk after next -> MLP -> that claim's result.
+        // With them all at the top, any wait hipcc puts there is for operations a whole chunk old
+        // (it merges wait counts over the loop's paths conservatively: with stores at the end of the
+        // previous iteration it waited for their round trip to memory before every chunk).
+        float pv[2] = {0.0f, 0.0f};
+        int pbase = n;  // the previous chunk (none: its stores fall past Y's end and are dropped)
         auto body = [&]() {
-            base = __builtin_amdgcn_readfirstlane(base);  // uniform: SGPRs, scalar branches
+            // everything in flight was issued a chunk ago: wait for it all here (free), so that
+            // hipcc's scoreboard holds nothing older than this iteration's own requests
+            __builtin_amdgcn_s_waitcnt(0x0f70);
+            const int base = cur * 128;
             const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
-            load((uint32_t)(base + stride2 + lane), nx[0], ny[0], nz[0], nf[0]);
-            load((uint32_t)(base + stride2 + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
-            float v[2];
+            const int nb = (nxt < 0 ? (int)nch : nxt) * 128;  // past the last chunk: zeros, unused
+            load((uint32_t)(nb + lane), nx[0], ny[0], nz[0], nf[0]);
+            load((uint32_t)(nb + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
+            store((uint32_t)(pbase + lane), pv[0]);
+            store((uint32_t)(pbase + 64 + lane), pv[1]);
+            const bool more = nxt >= 0;
+            const int ahead = (M.queue && more) ? claim() : 0;
 #if NR_MLP16_STAMPS
             const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
@@ -816,35 +887,36 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                             __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
                             __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
             else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
 #if NR_MLP16_STAMPS
             st_mlp += __builtin_amdgcn_s_memtime() - ta;
             ++st_n;
 #endif
-            store((uint32_t)(base + lane), v[0]);
-            store((uint32_t)(base + 64 + lane), v[1]);
+            pbase = base;
+            cur = nxt;
+            nxt = !more ? -1 : (M.queue ? settle(ahead) : fixed());
         };
 #if NR_MLP16_STAMPS
-        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (base < nfull) {
-            body();
-            for (base += stride2; base < nfull; base += stride2) body();
-        }
+        while (cur >= 0) body();
+        store((uint32_t)(pbase + lane), pv[0]);
+        store((uint32_t)(pbase + 64 + lane), pv[1]);
 #if NR_MLP16_STAMPS
         // diagnostic build: per wave {cycles in the loop, of them in the MLP calls, chunks} in Y
-        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) {
             Y[4 * wave] = (float)(t1 - t0);
             Y[4 * wave + 1] = (float)st_mlp;
             Y[4 * wave + 2] = (float)st_n;
+            Y[4 * wave + 3] = (float)(r1 - r0);  // 100 MHz ticks
         }
         return;
 #endif
-        // the ragged last chunk (1-127 points): the wave the grid-stride order gives it
-        if (nfull < n && (nfull >> 7) % waves == wave) {
+        // the ragged last chunk (1-127 points): the last wave of the grid
+        if (nfull < n && wave == waves - 1) {
             float x[2], y[2], z[2], f[2];
             load((uint32_t)(nfull + lane), x[0], y[0], z[0], f[0]);
             load((uint32_t)(nfull + 64 + lane), x[1], y[1], z[1], f[1]);
@@ -906,8 +978,12 @@ hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int
     return hipGetLastError();
 }
 
-hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
-    const int sm = smem16_bytes(M, prec, false);
+hipError_t launch_mlp16(const MlpArgs &M0, int prec, const float *X, float *Y, long n, int grid, int cus,
+                        uint32_t *queue, hipStream_t st) {
+    const int sm = smem16_bytes(M0, prec, false);
+    const bool lowp = prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16;
+    MlpArgs M = M0;
+    M.queue = (grid == 0 && lowp) ? queue : nullptr;
     // segments of at most 2^26 points: the kernel's buffer offsets (n * in0 * 4 bytes) are 32-bit
     constexpr long SEG = 1l << 26;
     for (long p0 = 0; p0 < n; p0 += SEG) {
@@ -915,9 +991,18 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         const float *x = X + p0 * M.in0;
         float *y = Y + p0;
         // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane)
-        const long per_wg = (prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16) ? 512 : 256;
-        const int g = (int)std::min<long>(grid, ((long)m + per_wg - 1) / per_wg);
-        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
+        const long per_wg = lowp ? 512 : 256;
+        auto go = [&](auto kern) {
+            int g = grid;
+            if (g <= 0) {  // persistent: the workgroups that fit at once (12 per CU without a queue)
+                int per_cu = 12;
+                if (M.queue && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, sm) != hipSuccess) per_cu = 3;
+                g = std::max(1, per_cu) * std::max(1, cus);
+            }
+            g = (int)std::max<long>(1, std::min<long>(g, ((long)m + per_wg - 1) / per_wg));
+            if (M.queue && hipMemsetAsync(M.queue, 0, NR_MLP16_QSHARDS * 128, st) != hipSuccess) return;
+            hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m);
+        };
         const bool four = M.in0 == 4;
         if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
         else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
