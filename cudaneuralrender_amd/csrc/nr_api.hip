@@ -51,7 +51,6 @@ struct nr_ctx {
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
-    uint32_t *d_mlpq = nullptr;  // k_mlp16's chunk queue (up to 32 counters on 128-byte lines)
     int debug = 0;
     int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
     // temporal block ordering (nr_set_temporal_order)
@@ -724,7 +723,7 @@ int nr_destroy(nr_ctx *c) {
     if (!(c->use_own && !c->own_stream)) (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap); dfree(c->d_mlpq);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
     dfree(c->d_frames); dfree(c->d_bout);
     if (c->h_frames) (void)hipHostFree(c->h_frames);
@@ -1218,17 +1217,13 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // 12 workgroups per CU by default: more than fit at once (3-5), so that workgroups start
         // staggered as earlier ones retire -- a grid of exactly the resident workgroups runs the
         // bf16 MLP 17 % slower (its waves stay in step: profiles/r3_mlp_bpc.txt)
-        // nr_set_occupancy(bpc > 0): bpc workgroups per CU in the fixed grid-stride order; by default
-        // bf16/fp16 run a persistent grid fed by the chunk queue, the others 12 per CU (queued
-        // beyond the resident ones)
-        const int cus = num_cus(c->device);
-        const int grid = c->blocks_per_cu > 0 ? cus * c->blocks_per_cu : 0;
-        if (!c->d_mlpq) HIPCHK(c, hipMalloc(&c->d_mlpq, 32 * 128));
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 12;
+        const int grid = num_cus(c->device) * bpc;
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, c->precision, dX, dY, (int)n,
                                          ((c->wave_rays > 0 ? c->wave_rays : 64) + 15) / 16, (c->debug >> 7) & 1, s));
         else
-            HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, grid, cus, c->d_mlpq, s));
+            HIPCHK(c, launch_mlp16(c->mlp16, c->precision, dX, dY, n, grid, s));
     } else {
         float *bufs[2] = {scratch, scratch + (size_t)chunk * maxw};
         const int cus = num_cus(c->device);

@@ -18,8 +18,6 @@ struct MlpArgs {
                             // waves whose inputs are all within F32_INPUT_BOUND
     int lp_stream;          // 16-bit MLP as the pipelined streams of nr_mlp16_asm.h (7 hidden
                             // layers); 0 (nr_set_debug bit 11): the builtin form, same values
-    uint32_t *queue;        // k_mlp16's chunk queue (counters on 128-byte lines), or NULL:
-                            // the fixed grid-stride order
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
@@ -128,10 +126,7 @@ hipError_t launch_init_l(const RenderArgs *Ad, const QueueArgs &Q, long npix, hi
 hipError_t launch_march_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf, int it, int grid, hipStream_t st);
 hipError_t launch_shade_l(const RenderArgs *Ad, const QueueArgs &Q, const float *sdf4, int grid, hipStream_t st);
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st);
-// grid > 0: that many workgroups in the fixed grid-stride order; grid == 0: a persistent grid of
-// the resident workgroups (cus CUs) dealt chunks by the queue (bf16/fp16; queue: 4 KiB of device memory)
-hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, int cus,
-                        uint32_t *queue, hipStream_t st);
+hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st);
 hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float *Y, int reps, int nt, int part,
                               hipStream_t st);
 hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int bw, int dilate, hipStream_t st);

@@ -710,12 +710,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 #ifndef NR_MLP16_STAMPS
 #define NR_MLP16_STAMPS 0
 #endif
-// counters of k_mlp16's chunk queue (a power of two): one word serves ~88 atomics per us
-// (MI355X_MICROARCH.md 'dequeue'), and a 2^24-point bf16 launch takes ~800 chunks per us
-#ifndef NR_MLP16_QSHARDS
-#define NR_MLP16_QSHARDS 16
-#endif
-static_assert((NR_MLP16_QSHARDS & (NR_MLP16_QSHARDS - 1)) == 0 && NR_MLP16_QSHARDS <= 32, "queue shards");
 // waves per SIMD k_mlp16's registers target (<= 96 VGPRs at 5)
 #ifndef NR_MLP16_WPS
 #define NR_MLP16_WPS 5
@@ -804,52 +798,17 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         unsigned long long st_mlp = 0;
         uint32_t st_n = 0;
 #endif
-        // The whole chunks are dealt by a queue (M.queue: NR_MLP16_QSHARDS counters, one per 128-byte
-        // line, zeroed before the launch) to a persistent grid: shard s holds chunks s, s + Q, s + 2Q,
-        // ... (Q shards); a wave takes one chunk of its shard per atomic and moves to the next shard
-        // once its own is dry.  Dealt this way, a SIMD that runs slower (clock, placement) takes
-        // fewer chunks: with a fixed grid-stride share the last wave of a launch ended 13 % after the
-        // median one (tools/mlp_stamps.py).  The indices run two chunks ahead: the claim for chunk
-        // i + 2 is issued at the top of chunk i and read at its end, so its ~1-2 us round trip hides
-        // under the MLP with no branch in between.  The atomic is a buffer atomic every lane issues,
-        // lanes 1-63 at an offset past the buffer (dropped by the range check): no lane-divergent
-        // branch, whose join would wait for the return at once.
-        // M.queue == nullptr: the fixed grid-stride order (a wave's chunks wave, wave + waves, ...).
-        constexpr int Q = NR_MLP16_QSHARDS;
+        // Grid-stride chunks: a wave's chunks are wave, wave + waves, ...  (A queue dealing chunks
+        // to a persistent grid by atomics measured slower: the claims' round trips, ~2,500 cycles
+        // per chunk under load, outweighed the balance they bought; profiles/r4_mlp_queue.txt.)
         const uint32_t nch = (uint32_t)(nfull >> 7);
-        const auto rq = buffer_of(M.queue, (uint32_t)Q * 128u);
-        const uint32_t qlane = lane == 0 ? 0u : 0x7fffff00u;
-        int sh = wave & (Q - 1), tries = 0, gs = wave;
-        auto claim = [&]() -> int {  // issued, not waited for (lane 0 holds the position)
-            return __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, (int)(qlane + (uint32_t)sh * 128u), 0, 0);
-        };
-        auto shard_n = [&](int s) -> uint32_t {
-            return nch > (uint32_t)s ? (nch - 1u - (uint32_t)s) / (uint32_t)Q + 1u : 0u;
-        };
-        // the chunk of claim result r (lane 0's position in shard sh); past the shard: the next
-        // shards, by blocking claims; -1 when every shard is dry (wave-uniform)
-        auto settle = [&](int r) -> int {
-            uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(r);
-            while (v >= shard_n(sh)) {
-                if (++tries >= Q) return -1;
-                sh = (sh + 1) & (Q - 1);
-                v = (uint32_t)__builtin_amdgcn_readfirstlane(claim());
-            }
-            return (int)(v * (uint32_t)Q + (uint32_t)sh);
-        };
+        int gs = wave;
         auto fixed = [&]() -> int {
             const int c = gs;
             gs += waves;
             return c < (int)nch ? c : -1;
         };
-        int cur, nxt;
-        if (M.queue) {
-            cur = settle(claim());
-            nxt = cur < 0 ? -1 : settle(claim());
-        } else {
-            cur = fixed();
-            nxt = fixed();
-        }
+        int cur = fixed(), nxt = fixed();
         float nx[2], ny[2], nz[2], nf[2];
         const int c0 = cur < 0 ? (int)nch : cur;
         load((uint32_t)(c0 * 128 + lane), nx[0], ny[0], nz[0], nf[0]);
@@ -860,8 +819,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         __builtin_amdgcn_s_waitcnt(0x0f70);
         // One chunk: wait for its inputs (requested one chunk earlier) -> every memory operation of
         // the iteration: the next chunk's input loads, the previous chunk's stores (its outputs were
-        // kept in registers), the claim for the chunk after next -> MLP -> that claim's result.
-        // With them all at the top, any wait hipcc puts there is for operations a whole chunk old
+        // kept in registers) -> MLP.  With them all at the top, any wait hipcc puts there is for operations a whole chunk old
         // (it merges wait counts over the loop's paths conservatively: with stores at the end of the
         // previous iteration it waited for their round trip to memory before every chunk).
         float pv[2] = {0.0f, 0.0f};
@@ -877,8 +835,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             load((uint32_t)(nb + 64 + lane), nx[1], ny[1], nz[1], nf[1]);
             store((uint32_t)(pbase + lane), pv[0]);
             store((uint32_t)(pbase + 64 + lane), pv[1]);
-            const bool more = nxt >= 0;
-            const int ahead = (M.queue && more) ? claim() : 0;
 #if NR_MLP16_STAMPS
             const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
@@ -896,7 +852,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
 #endif
             pbase = base;
             cur = nxt;
-            nxt = !more ? -1 : (M.queue ? settle(ahead) : fixed());
+            nxt = fixed();
         };
 #if NR_MLP16_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -978,12 +934,9 @@ hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int
     return hipGetLastError();
 }
 
-hipError_t launch_mlp16(const MlpArgs &M0, int prec, const float *X, float *Y, long n, int grid, int cus,
-                        uint32_t *queue, hipStream_t st) {
-    const int sm = smem16_bytes(M0, prec, false);
+hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
+    const int sm = smem16_bytes(M, prec, false);
     const bool lowp = prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16;
-    MlpArgs M = M0;
-    M.queue = (grid == 0 && lowp) ? queue : nullptr;
     // segments of at most 2^26 points: the kernel's buffer offsets (n * in0 * 4 bytes) are 32-bit
     constexpr long SEG = 1l << 26;
     for (long p0 = 0; p0 < n; p0 += SEG) {
@@ -992,17 +945,8 @@ hipError_t launch_mlp16(const MlpArgs &M0, int prec, const float *X, float *Y, l
         float *y = Y + p0;
         // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane)
         const long per_wg = lowp ? 512 : 256;
-        auto go = [&](auto kern) {
-            int g = grid;
-            if (g <= 0) {  // persistent: the workgroups that fit at once (12 per CU without a queue)
-                int per_cu = 12;
-                if (M.queue && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, sm) != hipSuccess) per_cu = 3;
-                g = std::max(1, per_cu) * std::max(1, cus);
-            }
-            g = (int)std::max<long>(1, std::min<long>(g, ((long)m + per_wg - 1) / per_wg));
-            if (M.queue && hipMemsetAsync(M.queue, 0, NR_MLP16_QSHARDS * 128, st) != hipSuccess) return;
-            hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m);
-        };
+        const int g = (int)std::max<long>(1, std::min<long>(grid, ((long)m + per_wg - 1) / per_wg));
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
         const bool four = M.in0 == 4;
         if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
         else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
