@@ -39,6 +39,7 @@ struct File {
         for (int i = n - 1; i >= 0; --i) v = (v << 8) | d[off + i];
         return v;
     }
+    uint8_t byte(uint64_t off) const { return (uint8_t)uint(off, 1); }
     uint64_t addr(uint64_t off) const { return uint(off, so); }
     bool undef(uint64_t a) const { return so == 8 ? a == ~0ull : a == ((1ull << (8 * so)) - 1); }
     uint64_t abs(uint64_t a) const { return base + a; }
@@ -70,7 +71,7 @@ std::vector<Msg> object_messages(const File &f, uint64_t oh_addr) {
             Msg m;
             m.type = (uint16_t)f.uint(q, 2);
             m.size = (uint32_t)f.uint(q + 2, 2);
-            m.flags = f.d[q + 4];
+            m.flags = f.byte(q + 4);
             m.off = q + 8;
             f.need(m.off, m.size);
             if (m.type == 0x10) {  // continuation
@@ -90,8 +91,9 @@ const Msg *find(const std::vector<Msg> &ms, uint16_t type) {
 
 struct Entry { std::string name; uint64_t oh; };
 
-void walk_btree(const File &f, uint64_t node, uint64_t heap_data, std::vector<Entry> &out, int depth) {
+void walk_btree(const File &f, uint64_t node, uint64_t heap_data, std::vector<Entry> &out, int depth, int &budget) {
     if (depth > 32) fail(NR_E_FORMAT, "HDF5: B-tree too deep");
+    if (--budget < 0) fail(NR_E_FORMAT, "HDF5: B-tree has too many nodes (a cycle?)");
     uint64_t p = f.abs(node);
     f.need(p, 8);
     if (memcmp(&f.d[p], "TREE", 4) != 0) fail(NR_E_FORMAT, "HDF5: bad B-tree signature");
@@ -103,7 +105,7 @@ void walk_btree(const File &f, uint64_t node, uint64_t heap_data, std::vector<En
     for (int i = 0; i < used; ++i) {
         uint64_t child = f.addr(q);
         q += f.so + f.sl;            // child, key i+1
-        if (level > 0) { walk_btree(f, child, heap_data, out, depth + 1); continue; }
+        if (level > 0) { walk_btree(f, child, heap_data, out, depth + 1, budget); continue; }
         uint64_t s = f.abs(child);
         f.need(s, 8);
         if (memcmp(&f.d[s], "SNOD", 4) != 0) fail(NR_E_FORMAT, "HDF5: bad symbol-node signature");
@@ -133,7 +135,8 @@ bool group_members(const File &f, uint64_t oh, std::vector<Entry> &out) {
     f.need(h, 8 + 2 * f.sl + f.so);
     if (memcmp(&f.d[h], "HEAP", 4) != 0) fail(NR_E_FORMAT, "HDF5: bad local heap signature");
     uint64_t heap_data = f.addr(h + 8 + 2 * f.sl);
-    walk_btree(f, btree, heap_data, out, 0);
+    int budget = 4096;
+    walk_btree(f, btree, heap_data, out, 0, budget);
     std::stable_sort(out.begin(), out.end(), [](const Entry &a, const Entry &b) {
         return strcmp(a.name.c_str(), b.name.c_str()) < 0;
     });
@@ -157,23 +160,28 @@ DsInfo dataset_info(const File &f, uint64_t oh) {
     if (ty->flags & 0x02) fail(NR_E_FORMAT, "HDF5: shared (committed) datatypes unsupported");
     if (find(ms, 0x0B)) fail(NR_E_FORMAT, "HDF5: filtered datasets unsupported");
     DsInfo I;
-    // dataspace
-    int sv = f.d[sp->off], nd = f.d[sp->off + 1];
+    // dataspace (every field read through a bounds-checked accessor: a message may be shorter than
+    // its type's layout in a damaged file)
+    int sv = f.byte(sp->off), nd = f.byte(sp->off + 1);
     uint64_t dp = (sv == 1) ? sp->off + 8 : (sv == 2 ? sp->off + 4 : 0);
     if (!dp) fail(NR_E_FORMAT, "HDF5: unknown dataspace version");
     I.dims.resize(nd);
-    for (int i = 0; i < nd; ++i) { I.dims[i] = f.uint(dp + (uint64_t)i * f.sl, f.sl); I.count *= I.dims[i]; }
+    for (int i = 0; i < nd; ++i) {
+        I.dims[i] = f.uint(dp + (uint64_t)i * f.sl, f.sl);
+        // no product past 2^31 elements (a file is at most 1 GiB): the byte count cannot wrap
+        if (I.dims[i] > (1ull << 31) || (I.count *= I.dims[i]) > (1ull << 31)) fail(NR_E_FORMAT, "HDF5: dataset too large");
+    }
     // datatype
-    int cls = f.d[ty->off] & 0x0f;
-    uint8_t bits0 = f.d[ty->off + 1];
+    int cls = f.byte(ty->off) & 0x0f;
+    uint8_t bits0 = f.byte(ty->off + 1);
     I.esz = (uint32_t)f.uint(ty->off + 4, 4);
     if (cls != 1 || (I.esz != 4 && I.esz != 8)) fail(NR_E_FORMAT, "HDF5: dataset is not IEEE float32/float64");
     I.be = bits0 & 1;
     // layout
-    int lv = f.d[lay->off];
+    int lv = f.byte(lay->off);
     const uint64_t data_len = I.count * I.esz;
     if (lv == 3 || lv == 4) {
-        int lc = f.d[lay->off + 1];
+        int lc = f.byte(lay->off + 1);
         if (lc == 1) {
             uint64_t a = f.addr(lay->off + 2);
             I.undefined = f.undef(a);
@@ -186,7 +194,7 @@ DsInfo dataset_info(const File &f, uint64_t oh) {
             fail(NR_E_FORMAT, "HDF5: chunked/virtual datasets unsupported");
         }
     } else if (lv == 1 || lv == 2) {
-        int lnd = f.d[lay->off + 1], lc = f.d[lay->off + 2];
+        int lnd = f.byte(lay->off + 1), lc = f.byte(lay->off + 2);
         if (lc == 1) {
             uint64_t a = f.addr(lay->off + 8);
             I.undefined = f.undef(a);
@@ -244,10 +252,12 @@ void open_file(const char *path, File &f) {
     }
     if (sb == ~0ull) fail(NR_E_FORMAT, "not an HDF5 file");
     f.sb = sb;
-    int ver = f.d[sb + 8];
+    int ver = f.byte(sb + 8);
     if (ver > 1) fail(NR_E_FORMAT, "HDF5: superblock version >1 unsupported");
-    f.so = f.d[sb + 13];
-    f.sl = f.d[sb + 14];
+    f.so = f.byte(sb + 13);
+    f.sl = f.byte(sb + 14);
+    if ((f.so != 2 && f.so != 4 && f.so != 8) || (f.sl != 2 && f.sl != 4 && f.sl != 8))
+        fail(NR_E_FORMAT, "HDF5: bad offset/length sizes in the superblock");
     if ((f.so != 4 && f.so != 8) || (f.sl != 4 && f.sl != 8)) fail(NR_E_FORMAT, "HDF5: odd offset size");
     uint64_t p = sb + 24 + (ver == 1 ? 4 : 0);
     f.base = f.addr(p);
@@ -256,7 +266,7 @@ void open_file(const char *path, File &f) {
 
 uint64_t root_object(const File &f) {
     // the root symbol-table entry follows the 4 addresses of the superblock
-    const int ver = f.d[f.sb + 8];
+    const int ver = f.byte(f.sb + 8);
     const uint64_t rootent = f.sb + 24 + (ver == 1 ? 4 : 0) + 4 * (uint64_t)f.so;
     return f.addr(rootent + f.so);
 }
