@@ -31,8 +31,9 @@ __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__re
 
 // The same for the 16-bit MLP on 128 points (k_mlp16's form, mlp32_lowp_128; 7 hidden layers):
 // PART 0 = the whole evaluation (the stream if M.lp_stream, else the builtin form), PART 1 = the
-// pipelined stream alone (nr_mlp16_asm.h), its outputs fed back as its inputs.  Y[0] = shader
-// cycles per 128-point evaluation.
+// pipelined stream alone (nr_mlp16_asm.h), its outputs fed back as its inputs; and on the
+// tracer's 64 points (mlp16_lowp, one point per lane): PART 2 = two 32-point tiles (the two-tile
+// stream if M.lp_stream), PART 3 = one.  Y[0] = shader cycles per evaluation.
 template <int PREC, int PART>
 __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
                                                        int reps) {
@@ -55,6 +56,9 @@ __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *_
         if constexpr (PART == 0) {
             const float xr[2] = {x[0] + v[0] * 1e-30f, x[1] + v[1] * 1e-30f};
             mlp32_lowp_128<PREC, 7, CL>(slp, sfl, M.in0, 7, fr, xr, y, z, v, M.lp_stream != 0);
+        } else if constexpr (PART >= 2) {
+            v[0] = mlp16_lowp<PREC>(slp, sfl, M.in0, 7, 0.0f, x[0] + v[0] * 1e-30f, y[0], z[0], PART == 2 ? 0xfu : 0x3u, CL,
+                                    M.lp_stream != 0);
         } else {
             mlp7_x4_stream<PREC, CL>(slp, sfl, kk);
             for (int t = 0; t < 4; ++t) kk[t][0] = kk[t][1] & 0x3f003f00u;
@@ -63,7 +67,7 @@ __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *_
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
-    Y[1 + lane] = PART == 0 ? v[0] + v[1] : __uint_as_float(kk[0][0][0] ^ kk[3][1][3]);
+    Y[1 + lane] = PART == 0 ? v[0] + v[1] : PART >= 2 ? v[0] : __uint_as_float(kk[0][0][0] ^ kk[3][1][3]);
 }
 
 template <int PART>
@@ -81,8 +85,19 @@ hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float 
         if (M.nh != 7 || M.in0 != 3 || !M.lp) return hipErrorInvalidValue;
         const int sm = M.lp_bytes + M.lpf_bytes;
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(1), dim3(64), sm, st, M, X, Y, reps); };
-        if (prec == NR_PRECISION_BF16) part ? go(k_mlp_latency_lp<NR_PRECISION_BF16, 1>) : go(k_mlp_latency_lp<NR_PRECISION_BF16, 0>);
-        else part ? go(k_mlp_latency_lp<NR_PRECISION_FP16, 1>) : go(k_mlp_latency_lp<NR_PRECISION_FP16, 0>);
+        // nt <= 2: the tracer's 64-point form on nt 32-point tiles; else k_mlp16's 128 points
+        const int pt = part ? 1 : nt == 1 ? 3 : nt == 2 ? 2 : 0;
+        if (prec == NR_PRECISION_BF16) {
+            if (pt == 0) go(k_mlp_latency_lp<NR_PRECISION_BF16, 0>);
+            else if (pt == 1) go(k_mlp_latency_lp<NR_PRECISION_BF16, 1>);
+            else if (pt == 2) go(k_mlp_latency_lp<NR_PRECISION_BF16, 2>);
+            else go(k_mlp_latency_lp<NR_PRECISION_BF16, 3>);
+        } else {
+            if (pt == 0) go(k_mlp_latency_lp<NR_PRECISION_FP16, 0>);
+            else if (pt == 1) go(k_mlp_latency_lp<NR_PRECISION_FP16, 1>);
+            else if (pt == 2) go(k_mlp_latency_lp<NR_PRECISION_FP16, 2>);
+            else go(k_mlp_latency_lp<NR_PRECISION_FP16, 3>);
+        }
         return hipGetLastError();
     }
     if (part) launch_lat<1>(M, X, Y, reps, nt, st);

@@ -478,15 +478,91 @@ __device__ __forceinline__ float hi16f(uint32_t p) {
     else return (float)__builtin_bit_cast(_Float16, (uint16_t)(p >> 16));
 }
 
+// The pipelined streams (nr_mlp16_asm.h, tools/gen_mlp_asm.py) for the 7-hidden-layer networks:
+// 1 = on (MlpArgs::lp_stream, cleared by nr_set_debug bit 11, selects them at run time), 0 = never
+#ifndef NR_LP_STREAM
+#define NR_LP_STREAM 1
+#endif
+
+// LDS byte address of a pointer into shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// Input layer + 7 hidden layers + the final layer's operand conversion of two 32-point tiles (the
+// tracer's 64 points) as one software-pipelined stream: tile 1's conversions beside tile 0's MFMAs,
+// the next layer's tile 0 beside tile 1's, every layer's operands read one layer ahead into the
+// idle one of two register buffers (nr_mlp16_asm.h NR_HID7X2_*).  In: k[t][0] = tile t's
+// input-layer B operand; out: k[t][s] = the final layer's ReLU'd B operands -- relu_pack_tiles'
+// values after hidden_layers, bit for bit.  Registers pinned to v0-v95.
+template <int PREC, bool CL>
+__device__ __forceinline__ void mlp7_x2_stream(const uint16_t *__restrict__ lp, const float *__restrict__ fl,
+                                               u32x4 (&k)[2][2]) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const int lane = lane_id();
+    const uint32_t va = lds_addr(lp) + 16u * (uint32_t)lane, vb = lds_addr(fl) + 64u * (uint32_t)(lane >> 5);
+    f32x16 c0, c1, bb0, bb1;
+    u32x8 ab0, ab1;
+#define NR_STREAM_OPERANDS                                                                                          \
+    : "+{v[32:35]}"(k[0][0]), "=&{v[36:39]}"(k[0][1]), "+{v[40:43]}"(k[1][0]), "=&{v[44:47]}"(k[1][1]),            \
+      "=&{v[0:15]}"(c0), "=&{v[16:31]}"(c1), "=&{v[48:55]}"(ab0), "=&{v[56:63]}"(ab1), "=&{v[64:79]}"(bb0),         \
+      "=&{v[80:95]}"(bb1)                                                                                          \
+    : [va] "v"(va), [vb] "v"(vb)                                                                                   \
+    : "memory"
+    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_HID7X2_BF16_CLAMP NR_STREAM_OPERANDS);
+    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_HID7X2_BF16_MAX NR_STREAM_OPERANDS);
+    else asm volatile(NR_HID7X2_F16_MAX NR_STREAM_OPERANDS);
+#undef NR_STREAM_OPERANDS
+}
+
 // CL: ReLU by the conversion's clamp (bf16 with the clamped pack, inputs within
-// LP_INPUT_BOUND -- the caller checks); otherwise cvt + v_pk_max_i16 (any pack, any input)
+// LP_INPUT_BOUND -- the caller checks); otherwise cvt + v_pk_max_i16 (any pack, any input).
+// stream: two tiles of a 7-hidden-layer network take the pipelined stream (mlp7_x2_stream).
 template <int PREC, int NT, int NH, bool CL>
 __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                               int nh_rt, float fr, float x, float y, float z) {
+                                               int nh_rt, float fr, float x, float y, float z, bool stream = false) {
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
     f32x16 acc[NT];
+    if constexpr (NR_LP_STREAM && NT == 2 && NH == 7) {
+        if (stream) {
+            // the input layer's B operands exactly as below, then the stream, then the final layer
+            const uint32_t p0 = cvt2<PREC>(x, y);
+            const float dx = x - lo16f<PREC>(p0), dy = y - hi16f<PREC>(p0);
+            const uint32_t q = cvt2<PREC>(z, dx);
+            const uint32_t r = cvt2<PREC>(dy, z - lo16f<PREC>(q));
+            uint32_t f = 0;
+            if (in0 == 4) {
+                const uint32_t f0 = cvt2<PREC>(fr, 0.0f);
+                f = cvt2<PREC>(fr, fr - lo16f<PREC>(f0));
+            }
+            const uint32_t qf = (q & 0xffffu) | (f << 16);
+            const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
+            const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
+            const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
+            const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
+            u32x4 kk[2][2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) kk[t][0] = (u32x4){w0[t], w1[t], w2[t], w3[t]};
+            mlp7_x2_stream<PREC, CL>(lp, fl, kk);
+            const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(7));
+            const u32x4 wf[2] = {F4[h], F4[2 + h]};
+            const float bf = fl[32 + 32 * 7];
+            float zt[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                float a = 0.0f;
+#pragma unroll
+                for (int st = 0; st < 2; ++st)
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) a = dot2<PREC>(kk[t][st][qq], wf[st][qq], a);
+                zt[t] = a;
+            }
+            const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
+            return (__uint_as_float(rr[0]) + __uint_as_float(rr[1])) + bf;
+        }
+    }
     {
         // B operand of tile t, lanes 0-31 (k 0-7) of point l: {xh, yh | zh, xl | yl, zl | fh, fl};
         // lanes 32-63 (k 8-15) of point l - 32: {xh, yh | zh, fh | 0 | 0}.  Each lane splits
@@ -562,20 +638,10 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
 #ifndef NR_LP_FINAL_MFMA
 #define NR_LP_FINAL_MFMA 0
 #endif
-// The pipelined stream (nr_mlp16_asm.h, tools/gen_mlp_asm.py) for the 7-hidden-layer networks:
-// 1 = on (MlpArgs::lp_stream, cleared by nr_set_debug bit 11, selects it at run time), 0 = never
-#ifndef NR_LP_STREAM
-#define NR_LP_STREAM 1
-#endif
 // A/B: issue priority NR_STREAM_PRIO outside the stream, 0 inside it (0 = no priority change)
 #ifndef NR_STREAM_PRIO
 #define NR_STREAM_PRIO 0
 #endif
-
-// LDS byte address of a pointer into shared memory
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
 
 // Input layer + 7 hidden layers + the final layer's operand conversion of four 32-point tiles as
 // one software-pipelined instruction stream: tile t + 1's conversions issue beside tile t's MFMAs
@@ -749,11 +815,12 @@ __device__ __forceinline__ void mlp128_lowp_cl(const uint16_t *__restrict__ lp, 
 
 template <int PREC, bool CL>
 __device__ __forceinline__ float mlp16_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                               int nh, float fr, float x, float y, float z, uint32_t tmask) {
+                                               int nh, float fr, float x, float y, float z, uint32_t tmask,
+                                               bool stream) {
     // the bundled networks' depth (7 hidden layers) fully unrolled: no loop-carried
     // accumulator copies between layers
     if (nh == 7) {
-        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
+        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7, CL>(lp, fl, in0, nh, fr, x, y, z, stream);
         return mlp32_lowp_nt<PREC, 1, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
     }
     if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 0, CL>(lp, fl, in0, nh, fr, x, y, z);
@@ -762,14 +829,16 @@ __device__ __forceinline__ float mlp16_lowp_cl(const uint16_t *__restrict__ lp, 
 
 // tmask: the caller's 16-point tiles (bits 0-3); the 32-point tiles cover pairs of them.
 // cl (wave-uniform): the clamped-ReLU form is valid -- the pack is clamped (M.lp_clamp) and
-// every input of the call is within LP_INPUT_BOUND.
+// every input of the call is within LP_INPUT_BOUND.  stream: M.lp_stream (two tiles of a
+// 7-hidden-layer network take the pipelined stream)
 template <int PREC>
 __device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                            int nh, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
+                                            int nh, float fr, float x, float y, float z, uint32_t tmask, bool cl,
+                                            bool stream) {
     if constexpr (PREC == NR_PRECISION_BF16) {
-        if (cl) return mlp16_lowp_cl<PREC, true>(lp, fl, in0, nh, fr, x, y, z, tmask);
+        if (cl) return mlp16_lowp_cl<PREC, true>(lp, fl, in0, nh, fr, x, y, z, tmask, stream);
     }
-    return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask);
+    return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask, stream);
 }
 
 // ---- fp32x3: fp32-class hidden layers on the fp16 matrix core (NR_PRECISION_FP32X3).
@@ -929,12 +998,21 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return in ? v3 : v32;
 }
 
+// The two-tile stream in the tracer's march (A/B knob, off): one wave alone runs the 64-point MLP
+// in 1,964 instead of 2,308 cycles, but the stream's 96 pinned registers push the tracer's live
+// state into scratch (bf16 batch: 8 -> 38 spilled VGPRs) and C3 runs 1.52 instead of 1.39 ms per
+// frame (profiles/r4_ab_stream.txt)
+#ifndef NR_TRACE_STREAM
+#define NR_TRACE_STREAM 0
+#endif
+
 // cl: see mlp16_lowp (ignored in fp32); fp32x3: the pack is valid (M.lp_clamp), the inputs are
 // checked here
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
-    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
-    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
+    const bool stream = NR_TRACE_STREAM && M.lp_stream != 0;
+    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl, stream);
+    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl, stream);
     if (prec == NR_PRECISION_FP32X3) return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0);
     return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }

@@ -79,3 +79,49 @@ def test_mlp_stream_ragged(rend, nets, prec):
             assert np.array_equal(a, b), n
     finally:
         rend.set_precision("fp32")
+
+
+# ---- the tracer's march MLP (two 32-point tiles per wave: mlp7_x2_stream) -- whole frames
+
+@pytest.fixture(scope="module")
+def chrome():
+    return nr.load_png(nr.matcap_path("Chrome"))
+
+
+@pytest.mark.parametrize("prec,debug", [("bf16", 0), ("bf16", NO_CLAMP), ("fp16", 0)])
+@pytest.mark.parametrize("geom", ["plane_1", "car_1"])
+def test_trace_stream_frames_identical(rend, chrome, geom, prec, debug):
+    """One frame and a 6-frame batch (the batched instance) with the stream and with the builtin
+    form: every pixel identical, and the same ray-step counts."""
+    rend.load_h5(nr.geometry_path(geom)).set_precision(prec)
+    rend.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+    cams = [nr.camera(5.0 * i, 30.0 * i, 2.0) + (i,) for i in range(6)]
+    rend.set_view(*cams[1][:2], 0)
+    try:
+        (a, sa), (b, sb) = stream_and_builtin(rend, lambda: rend.render(384, 320, 128), debug)
+        assert np.array_equal(a, b), int((a != b).sum())
+        assert sa["ray_steps"] == sb["ray_steps"]
+        (fa, _), (fb, _) = stream_and_builtin(rend, lambda: rend.render_batch(256, 256, cams, 96), debug)
+        for i, (x, y) in enumerate(zip(fa, fb)):
+            assert np.array_equal(x, y), (i, int((x != y).sum()))
+    finally:
+        rend.set_precision("fp32")
+
+
+def test_trace_stream_animation_frames_identical(rend, chrome):
+    """A 4-input network: the frame number rides in the stream's input operands."""
+    rng = np.random.default_rng(24)
+    dims = [4] + [32] * 8 + [1]
+    K = [(rng.standard_normal((dims[i], dims[i + 1])) / np.sqrt(dims[i])).astype(np.float32) for i in range(9)]
+    B = [(rng.standard_normal(dims[i + 1]) * 0.05).astype(np.float32) for i in range(9)]
+    B[-1][:] = 0.3
+    rend.load_mlp(dims, K, B).set_precision("bf16")
+    rend.set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
+    cams = [nr.camera(0.0, 10.0 * i, 2.0) + (7 * i,) for i in range(4)]
+    try:
+        (fa, sa), (fb, sb) = stream_and_builtin(rend, lambda: rend.render_batch(192, 160, cams, 64))
+        for i, (x, y) in enumerate(zip(fa, fb)):
+            assert np.array_equal(x, y), (i, int((x != y).sum()))
+        assert sa["ray_steps"] == sb["ray_steps"]
+    finally:
+        rend.set_static(nr.NR_COLOR_MATCAP, 3).set_precision("fp32")

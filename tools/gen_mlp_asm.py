@@ -1,5 +1,6 @@
 """Generates cudaneuralrender_amd/csrc/nr_mlp16_asm.h: the 16-bit MLP's hidden layers for four
-32-point tiles (128 points per wave, k_mlp16) as one software-pipelined instruction stream.
+32-point tiles (128 points per wave, k_mlp16) and for two (64 points, the tracer's march MLP:
+k_trace) as software-pipelined instruction streams.
 
 Why: compiled from builtins, every hidden layer issued its 8 MFMAs back to
 back and then converted all four tiles' accumulators (32 v_cvt_pk) with no MFMA in flight, so a
@@ -13,14 +14,18 @@ M(l,t,s) = v_mfma_f32_32x32x16_{bf16,f16} of layer l, tile t, k-step s (s = 0 ta
 its accumulator init, s = 1 the s = 0 result); C(l,t)s = the 4 v_cvt_pk (bf16: with the clamp bit
 that is the ReLU on the clamped pack; otherwise + v_pk_max_i16) that turn registers 8s..8s+7 of
 tile t's accumulator into the B operand of k-step s.  Every instruction and operand is the one the
-builtin form issues, so the outputs are bit-identical; only the order changes.
+builtin form issues, so the outputs are bit-identical; only the order changes.  With two tiles
+the same pattern puts the next layer's tile-0 conversions right behind tile 0's own MFMAs, so
+s_nop padding (inserted here wherever a distance falls short, then checked) covers the MFMA ->
+VALU distance the other two tiles' MFMAs covered.
 
 The stream runs inside one inline-asm statement, so the compiler neither pads its hazards nor
 counts its LDS reads: this script places the operand reads (ds_read_b128 of the next layer's A
 operands and biases into the idle one of two register buffers, one layer ahead) and CHECKS every
 hazard of the stream before it writes the header (check()).  The registers are pinned
-("{v[a:b]}" constraints): accumulators v0-v63, B operands v64-v95, A operands v96-v111, biases
-v112-v143.
+("{v[a:b]}" constraints), for NT tiles: accumulators v[0 : 16NT), B operands v[16NT : 24NT), A
+operands 16 from v[24NT], biases 32 from v[24NT + 16] (four tiles: v0-v63, v64-v95, v96-v111,
+v112-v143; two: v0-v31, v32-v47, v48-v63, v64-v95).
 
 Run:  python tools/gen_mlp_asm.py   (writes the header; the CPU test suite checks it is current)
 """
@@ -28,10 +33,24 @@ import os
 import sys
 
 NH = 7                       # hidden layers of the bundled networks (others take the builtin form)
-ACC = lambda t: 16 * t                     # accumulator of tile t: v[16t : 16t+15]
-KOP = lambda t, s: 64 + 8 * t + 4 * s      # B operand of tile t, k-step s: 4 registers
-AOP = lambda b, s: 96 + 8 * b + 4 * s      # A operand of buffer b, k-step s: 4 registers
-BIAS = lambda b: 112 + 16 * b              # bias (accumulator init) of buffer b: 16 registers
+
+
+class Layout:
+    """Pinned registers of an NT-tile stream."""
+    def __init__(self, nt):
+        self.nt = nt
+
+    def ACC(self, t):            # accumulator of tile t: v[16t : 16t+15]
+        return 16 * t
+
+    def KOP(self, t, s):         # B operand of tile t, k-step s: 4 registers
+        return 16 * self.nt + 8 * t + 4 * s
+
+    def AOP(self, b, s):         # A operand of buffer b, k-step s: 4 registers
+        return 24 * self.nt + 8 * b + 4 * s
+
+    def BIAS(self, b):           # bias (accumulator init) of buffer b: 16 registers
+        return 24 * self.nt + 16 + 16 * b
 
 # hazard distances (wait states = instructions issued between producer and consumer; s_nop N
 # counts N + 1).  MFMA_VALU_RAW: hipcc's own gfx950 padding of v_mfma_f32_32x32x16 -> VALU read
@@ -44,34 +63,64 @@ SRCAB_WAR = 8
 
 
 class Stream:
-    def __init__(self):
+    def __init__(self, nt=4):
         self.ins = []   # (text, kind, reads, writes, states)
+        self.nt = nt
 
     def add(self, text, kind, reads=(), writes=(), states=1):
         self.ins.append((text, kind, tuple(reads), tuple(writes), states))
+
+    def nop(self, need):
+        while need > 0:
+            n = min(need, 16)
+            self.add(f"s_nop {n - 1}", "nop", states=n)
+            need -= n
+
+    def pad(self, kind, reads=(), writes=()):
+        """Appends the s_nop an instruction of `kind` reading / writing these registers needs after
+        the stream so far (the distances check() enforces)."""
+        regs = [r if isinstance(r, int) else r[1] for r in reads]
+        need, dist = 0, 0
+        for text, k, rd, wr, states in reversed(self.ins):
+            if dist >= SRCC_WAR:
+                break
+            if k == "mfma" and kind != "mfma":
+                if any(r in wr for r in regs) or any(r in wr for r in writes):
+                    need = max(need, MFMA_VALU_RAW - dist)
+                for role, r in rd:
+                    if r in writes:
+                        need = max(need, (SRCC_WAR if role == "C" else SRCAB_WAR) - dist)
+            elif k == "valu" and kind == "mfma" and any(r in wr for r in regs):
+                need = max(need, VALU_MFMA_RAW - dist)
+            dist += states
+        self.nop(need)
 
 
 def rng(a, n):
     return range(a, a + n)
 
 
-def build(prec, clamp):
+def build(prec, clamp, nt=4):
     dt = "bf16" if prec == "bf16" else "f16"
-    st = Stream()
+    st = Stream(nt)
+    L = Layout(nt)
+    ACC, KOP, AOP, BIAS = L.ACC, L.KOP, L.AOP, L.BIAS
 
     def mfma(buf, t, s, layer0=False):
         d = ACC(t)
         a = AOP(buf, 0) if layer0 else AOP(buf, s)
         b = KOP(t, s)
         c = BIAS(buf) if (layer0 or s == 0) else ACC(t)
+        reads = [("A", r) for r in rng(a, 4)] + [("B", r) for r in rng(b, 4)] + [("C", r) for r in rng(c, 16)]
+        st.pad("mfma", reads, list(rng(d, 16)))
         st.add(f"v_mfma_f32_32x32x16_{dt} v[{d}:{d + 15}], v[{a}:{a + 3}], v[{b}:{b + 3}], v[{c}:{c + 15}]", "mfma",
-               reads=[("A", r) for r in rng(a, 4)] + [("B", r) for r in rng(b, 4)] + [("C", r) for r in rng(c, 16)],
-               writes=list(rng(d, 16)))
+               reads=reads, writes=list(rng(d, 16)))
 
     def conv(t, s):
         for q in range(4):
             src = ACC(t) + 8 * s + 2 * q
             dst = KOP(t, s) + q
+            st.pad("valu", [src, src + 1], [dst])
             if prec == "bf16" and clamp:
                 st.add(f"v_cvt_pk_bf16_f32 v{dst}, v{src}, v{src + 1} clamp", "valu", reads=[src, src + 1], writes=[dst])
             else:
@@ -81,6 +130,7 @@ def build(prec, clamp):
 
     def load(dst, addr, off):
         o = f" offset:{off}" if off else ""
+        st.pad("lds", (), list(rng(dst, 4)))
         st.add(f"ds_read_b128 v[{dst}:{dst + 3}], %[{addr}]{o}", "lds", writes=list(rng(dst, 4)))
 
     def a_loads(buf, j):       # hidden layer j's A operands (both k-steps) into buffer buf
@@ -101,9 +151,8 @@ def build(prec, clamp):
     mfma(0, 1, 0, layer0=True)
     for i in range(4):
         b_load(1, 0, i)
-    mfma(0, 2, 0, layer0=True)
-    mfma(0, 3, 0, layer0=True)
-    st.add("s_nop 3", "nop", states=4)
+    for t in range(2, nt):
+        mfma(0, t, 0, layer0=True)
     conv(0, 0)
     conv(0, 1)
     # ---- hidden layers l = 1..NH (hidden layer j = l - 1, buffer l % 2); the next layer's
@@ -111,11 +160,18 @@ def build(prec, clamp):
     for l in range(1, NH + 1):
         buf, j, nxt = l % 2, l - 1, l < NH
         wait()
-        for t in range(4):
+        for t in range(nt):
             for s in range(2):
                 mfma(buf, t, s)
-                conv(t + 1 if t < 3 else 0, s)   # tile t + 1 of this layer, or tile 0 of the next
-                if nxt:
+                conv(t + 1 if t < nt - 1 else 0, s)   # tile t + 1 of this layer, or tile 0 of the next
+                if nxt and nt == 2 and (t, s) == (0, 0):
+                    # two tiles: all of the next layer's operands right after this layer's first
+                    # MFMA -- a whole layer (4 MFMAs) ahead of their use; the other buffer's last
+                    # readers, the previous layer's tile-1 MFMAs, are just far enough back
+                    a_loads(1 - buf, j + 1)
+                    for i in range(4):
+                        b_load(1 - buf, j + 1, i)
+                elif nxt and nt == 4:
                     if (t, s) == (1, 0):
                         a_loads(1 - buf, j + 1)
                     elif (t, s) == (1, 1):
@@ -125,23 +181,31 @@ def build(prec, clamp):
                     elif (t, s) == (2, 1):
                         b_load(1 - buf, j + 1, 2)
                         b_load(1 - buf, j + 1, 3)
-    # ---- tail: the final layer's B operands of tiles 1-3 (tile 0's ran beside M(NH, 3, *))
-    for t in (1, 2, 3):
+    # ---- tail: the final layer's B operands of tiles 1.. (tile 0's ran beside M(NH, nt - 1, *)),
+    # then whatever padding the exit needs: no MFMA of the stream in flight when it ends
+    for t in range(1, nt):
         conv(t, 0)
         conv(t, 1)
+    dist, need = 0, 0
+    for text, k, rd, wr, states in reversed(st.ins):
+        if k == "mfma":
+            need = max(need, MFMA_VALU_RAW - dist, max(SRCC_WAR if role == "C" else SRCAB_WAR for role, _ in rd) - dist)
+        dist += states
+    st.nop(need)
     check(st)
     return st
 
 
 def check(st):
     """Verifies every hazard of the stream (raises on the first violation)."""
+    L = Layout(getattr(st, "nt", 4))
     pos = []   # wait-state position of each instruction
     p = 0
     for ins in st.ins:
         pos.append(p)
         p += ins[4]
     # the input B operands (k-step 0 slots) were written by the compiler's VALU just before the stream
-    last_w = {r: (-1, "valu") for t in range(4) for r in rng(KOP(t, 0), 4)}
+    last_w = {r: (-1, "valu") for t in range(L.nt) for r in rng(L.KOP(t, 0), 4)}
     last_r = {}      # reg -> list of (index, operand role) of MFMA reads since the last write
     pending = set()  # regs with an LDS load not yet waited for
     for i, (text, kind, reads, writes, _) in enumerate(st.ins):
@@ -212,15 +276,20 @@ def main():
         "// v[64+8t+4s:+3]; in: the input layer's B operands in k-step 0's slot; out: the ReLU'd final",
         "// operands), A operands v96-v111 and biases v112-v143 (two buffers each); %[va] = LDS byte",
         "// address of the A operands + 16 lane, %[vb] = of the biases + 64 (lane >> 5).",
+        "// NR_HID7X2_*: the same for two tiles (the tracer's 64 points): accumulators v0-v31, B operands",
+        "// v32-v47, A operands v48-v63, biases v64-v95.",
         "#pragma once",
         "",
     ]
-    for name, prec, clamp in (("NR_HID7_BF16_CLAMP", "bf16", True), ("NR_HID7_BF16_MAX", "bf16", False),
-                              ("NR_HID7_F16_MAX", "fp16", False)):
-        st = build(prec, clamp)
+    for name, prec, clamp, nt in (("NR_HID7_BF16_CLAMP", "bf16", True, 4), ("NR_HID7_BF16_MAX", "bf16", False, 4),
+                                  ("NR_HID7_F16_MAX", "fp16", False, 4), ("NR_HID7X2_BF16_CLAMP", "bf16", True, 2),
+                                  ("NR_HID7X2_BF16_MAX", "bf16", False, 2), ("NR_HID7X2_F16_MAX", "fp16", False, 2)):
+        st = build(prec, clamp, nt)
         nm = sum(1 for x in st.ins if x[1] == "mfma")
         nv = sum(1 for x in st.ins if x[1] == "valu")
-        parts.append(f"// {prec}, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, {nm} MFMA, {nv} VALU")
+        nn = sum(x[4] for x in st.ins if x[1] == "nop")
+        parts.append(f"// {prec}, {nt} tiles, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, {nm} MFMA, "
+                     f"{nv} VALU, {nn} s_nop states")
         parts.append(f"#define {name} \\")
         parts.append(emit(st).replace("\n", " \\\n") + "")
         parts.append("")

@@ -38,4 +38,16 @@ for prec in ("bf16", "fp16"):
         torch.cuda.synchronize()
         cyc = float(Y[0].item())
         print(f"{prec} 128 points {name:16s}: {cyc:.0f} cycles (60 MFMA issue floor {60 * 32})", flush=True)
+    # the tracer's form: 64 points, one per lane, on one or two 32-point tiles (wave_rays 16 / 32)
+    for nt in (2, 1):
+        r.set_wave_rays(16 * nt)
+        for flags, name in [(64, "stream"), (64 | 2048, "builtin")]:
+            r.set_debug(flags)
+            for _ in range(2):
+                r.mlp_forward_device(X2.data_ptr(), Y.data_ptr(), 2000)
+            torch.cuda.synchronize()
+            cyc = float(Y[0].item())
+            print(f"{prec} tracer form, {nt} tile(s) {name:8s}: {cyc:.0f} cycles (MFMA issue floor {30 * nt * 32 // 2})",
+                  flush=True)
+    r.set_wave_rays(0)
 r.set_debug(0)
