@@ -798,17 +798,40 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         unsigned long long st_mlp = 0;
         uint32_t st_n = 0;
 #endif
-        // Grid-stride chunks: a wave's chunks are wave, wave + waves, ...  (A queue dealing chunks
-        // to a persistent grid by atomics measured slower: the claims' round trips, ~2,500 cycles
-        // per chunk under load, outweighed the balance they bought; profiles/r4_mlp_queue.txt.)
+        // Grid-stride chunks: a wave's chunks are wave, wave + waves, ... up to nstat; the last
+        // M.dyn_eighths / 8 of the chunks are then claimed one at a time from a counter, so that
+        // the waves finish together whatever their clocks and neighbours (grid-stride alone: the
+        // slowest wave's loop ran 13 % past the median, profiles/r4_mlp_stream_stamps.txt).  A
+        // claim is requested at the top of the chunk whose end needs it and read at that end, a
+        // whole MLP later.  (A queue dealing every chunk by atomics measured slower: the claims'
+        // round trips, ~2,500 cycles per chunk under load; profiles/r4_mlp_queue.txt.)
         const uint32_t nch = (uint32_t)(nfull >> 7);
+        const uint32_t kst = M.dyn_eighths > 0 ? nch / 8u * (uint32_t)(8 - M.dyn_eighths) / (uint32_t)waves
+                                               : (nch + (uint32_t)waves - 1u) / (uint32_t)waves;
+        const int nstat = (int)min(nch, kst * (uint32_t)waves);
+        // the claim counter, lane 0 only (the others' offsets fall past the buffer and are dropped)
+        const auto rc = __builtin_amdgcn_make_buffer_rsrc(M.dyn_ctr, 0, 256, 0x00020000);
         int gs = wave;
+        uint32_t claim_v = 0;   // the claim requested at this chunk's top (lane 0)
+        bool dyn_end = M.dyn_eighths <= 0;   // no claims (any more): a claim came back past the last chunk
         auto fixed = [&]() -> int {
-            const int c = gs;
-            gs += waves;
-            return c < (int)nch ? c : -1;
+            if (gs < nstat) {
+                const int c = gs;
+                gs += waves;
+                return c;
+            }
+            if (dyn_end) return -1;
+            const int c = nstat + __builtin_amdgcn_readfirstlane((int)claim_v);
+            dyn_end = c >= (int)nch;
+            return dyn_end ? -1 : c;
         };
-        int cur = fixed(), nxt = fixed();
+        // the first two chunks: a wave with fewer than two static ones claims synchronously
+        auto first = [&]() -> int {
+            if (gs >= nstat && !dyn_end)
+                claim_v = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 ? 0 : 0x7fffff00, 0, 0);
+            return fixed();
+        };
+        int cur = first(), nxt = first();
         float nx[2], ny[2], nz[2], nf[2];
         const int c0 = cur < 0 ? (int)nch : cur;
         load((uint32_t)(c0 * 128 + lane), nx[0], ny[0], nz[0], nf[0]);
@@ -828,6 +851,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             // everything in flight was issued a chunk ago: wait for it all here (free), so that
             // hipcc's scoreboard holds nothing older than this iteration's own requests
             __builtin_amdgcn_s_waitcnt(0x0f70);
+            // the claim the end of this chunk reads (when its static chunks are used up): issued by
+            // every lane, lanes 1-63 and chunks that need none at an offset the buffer drops
+            const bool need = gs >= nstat && !dyn_end;
+            claim_v = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 && need ? 0 : 0x7fffff00, 0, 0);
             const int base = cur * 128;
             const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
             const int nb = (nxt < 0 ? (int)nch : nxt) * 128;  // past the last chunk: zeros, unused
@@ -860,6 +887,17 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         while (cur >= 0) body();
         store((uint32_t)(pbase + lane), pv[0]);
         store((uint32_t)(pbase + 64 + lane), pv[1]);
+        // the dynamic tail's counters back to zero for the next launch: by the last wave to finish
+        // (every wave's claims have returned by now)
+        if (M.dyn_eighths > 0) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const int done = __builtin_amdgcn_readfirstlane(
+                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 ? 128 : 0x7fffff00, 0, 0));
+            if (done == waves - 1) {
+                __builtin_amdgcn_raw_buffer_store_b32(0u, rc, lane == 0 ? 0 : 0x7fffff00, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(0u, rc, lane == 0 ? 128 : 0x7fffff00, 0, 0);
+            }
+        }
 #if NR_MLP16_STAMPS
         // diagnostic build: per wave {cycles in the loop, of them in the MLP calls, chunks} in Y
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -868,6 +906,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             Y[4 * wave + 1] = (float)st_mlp;
             Y[4 * wave + 2] = (float)st_n;
             Y[4 * wave + 3] = (float)(r1 - r0);  // 100 MHz ticks
+            // the loop's start and end on the chip's 100 MHz clock (low 24 bits), after the per-wave block
+            Y[4 * waves + 2 * wave] = (float)(r0 & 0xffffffull);
+            Y[4 * waves + 2 * wave + 1] = (float)(r1 & 0xffffffull);
         }
         return;
 #endif

@@ -125,3 +125,30 @@ def test_trace_stream_animation_frames_identical(rend, chrome):
         assert sa["ray_steps"] == sb["ray_steps"]
     finally:
         rend.set_static(nr.NR_COLOR_MATCAP, 3).set_precision("fp32")
+
+
+# ---- k_mlp16's dynamic tail (the last eighth of the chunks claimed from a counter)
+
+NO_DYN = 1 << 12
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_mlp_dynamic_tail_equals_grid_stride(rend, nets, prec):
+    """Every point evaluated exactly once whatever the split between grid-stride and claimed
+    chunks (all claimed below ~450 k points), the same values as the grid-stride launch (bit 12),
+    and the counters back at zero after every launch (repeated launches stay right)."""
+    dims, K, B = nets["car_1"]
+    rend.load_mlp(dims, K, B).set_precision(prec)
+    rng = np.random.default_rng(25)
+    try:
+        for n in (1, 129, 128 * 777 + 5, (1 << 18) + 77, (1 << 20) + 64, 3_000_001):
+            X = rng.uniform(-1.2, 1.2, size=(n, 3)).astype(np.float32)
+            rend.set_debug(NO_DYN)
+            ref = rend.mlp_forward(X)
+            rend.set_debug(0)
+            for rep in range(3):
+                a = rend.mlp_forward(X)
+                assert np.array_equal(a, ref), (n, rep, int((a != ref).sum()))
+    finally:
+        rend.set_debug(0)
+        rend.set_precision("fp32")

@@ -23,7 +23,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1 << 22)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--precision", default="all")
-ap.add_argument("--bpc", default="12", help="workgroups per CU (0: the library default, 12)")
+ap.add_argument("--bpc", default="0", help="workgroups per CU (0: the library default: 12, or for bf16/fp16 3 with the dynamic tail)")
 ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (A/B of the bf16 ReLU forms: 512)")
 a = ap.parse_args()
 X = np.random.default_rng(0).uniform(-1, 1, size=(a.n, 3)).astype(np.float32)

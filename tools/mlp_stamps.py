@@ -19,9 +19,9 @@ r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
 for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
     r.set_precision(prec)
-    for debug in (0, 2048):
+    for debug in (4096, 4096 | 2048):
         r.set_debug(debug)
-        for bpc in (0, 3, 12):
+        for bpc in (3, 12):
             r.set_occupancy(bpc)
             for _ in range(3):
                 Y.zero_()
@@ -41,11 +41,27 @@ for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
             st2 = Y[: 4 * waves].view(waves, 4).cpu().numpy().astype(np.float64)
             st2 = st2[st2[:, 2] > 0]
             clock = float(np.median(st2[:, 0] / (st2[:, 3] / 100e6))) / 1e9
+            # per XCD (workgroup b runs on XCD b % 8): loop start / end on the 100 MHz clock
+            se = Y[4 * waves: 6 * waves].view(waves, 2).cpu().numpy().astype(np.int64)
+            base = se[:, 0].min()
+            if se[:, 0].max() - base > (1 << 23):  # the low 24 bits wrapped inside the launch
+                se = (se - (1 << 23)) % (1 << 24)
+                base = se[:, 0].min()
+            t0, t1 = (se[:, 0] - base) / 1e2, (se[:, 1] - base) / 1e2  # us
+            xcd = (np.arange(waves) // 4) % 8
+            by_xcd = {int(x): [round(float(np.median(t1[xcd == x])), 1), round(float(t1[xcd == x].max()), 1),
+                               round(float(np.median(st2[xcd[: len(st2)] == x, 0] / np.maximum(st2[xcd[: len(st2)] == x, 2], 1))))]
+                      for x in range(8)}
+            slot = (np.arange(waves) % 4)
+            by_slot = {int(k): round(float(np.median(t1[slot == k])), 1) for k in range(4)}
             print(json.dumps({"precision": prec, "debug": debug, "bpc": bpc, "waves": int(len(st)),
                               "cycles_per_chunk_median": round(float(np.median(per))),
                               "mlp_cycles_per_chunk_median": round(float(np.median(mlp))),
                               "outside_mlp": round(float(np.median(per - mlp))),
                               "clock_GHz": round(clock, 3), "kernel_ms": round(ms, 4),
                               "loop_ms_max": round(float(st2[:, 3].max()) / 1e5, 4),
-                              "loop_ms_median": round(float(np.median(st2[:, 3])) / 1e5, 4)}), flush=True)
+                              "loop_ms_median": round(float(np.median(st2[:, 3])) / 1e5, 4),
+                              "start_us_max": round(float(t0.max()), 1), "end_us_p10_p50_p90_max":
+                              [round(float(np.percentile(t1, q)), 1) for q in (10, 50, 90, 100)],
+                              "by_xcd_end_median_max_us_cycles_per_chunk": by_xcd, "by_wave_slot_end_us": by_slot}), flush=True)
 r.set_debug(0)
