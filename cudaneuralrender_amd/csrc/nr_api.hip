@@ -47,6 +47,7 @@ struct nr_ctx {
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
     bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
     bool no_dyn = false;     // nr_set_debug bit 12: k_mlp16 (bf16/fp16) without the dynamic tail
+    bool force_dyn = false;  // nr_set_debug bit 13: with it (an eighth) whatever NR_MLP16_DYN says
     uint32_t *d_dyn = nullptr;  // its counters (MlpArgs::dyn_ctr), zero between launches
     bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
                             // on the same packs
@@ -1223,13 +1224,14 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // here, then by each launch's last wave)
         const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
         MlpArgs M = c->mlp16;
-        if (lowp && NR_MLP16_DYN > 0 && !c->no_dyn) {
+        const int dyn = c->force_dyn ? 1 : NR_MLP16_DYN;
+        if (lowp && dyn > 0 && !c->no_dyn) {
             if (!c->d_dyn) {
                 HIPCHK(c, hipMalloc(&c->d_dyn, 256));
                 HIPCHK(c, hipMemsetAsync(c->d_dyn, 0, 256, s));
             }
             M.dyn_ctr = c->d_dyn;
-            M.dyn_eighths = NR_MLP16_DYN;
+            M.dyn_eighths = dyn;
         }
         // (bf16/fp16 since round 4: the resident grid, 3 per CU -- with the pipelined stream it runs
         // 2^24 points in 0.218 against 0.232 ms at 12, profiles/r4_ab_dyn.txt)
@@ -1387,6 +1389,7 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
     c->no_dyn = (flags >> 12) & 1;
+    c->force_dyn = (flags >> 13) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;

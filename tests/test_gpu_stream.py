@@ -130,6 +130,7 @@ def test_trace_stream_animation_frames_identical(rend, chrome):
 # ---- k_mlp16's dynamic tail (the last eighth of the chunks claimed from a counter)
 
 NO_DYN = 1 << 12
+DYN = 1 << 13
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
@@ -145,7 +146,7 @@ def test_mlp_dynamic_tail_equals_grid_stride(rend, nets, prec):
             X = rng.uniform(-1.2, 1.2, size=(n, 3)).astype(np.float32)
             rend.set_debug(NO_DYN)
             ref = rend.mlp_forward(X)
-            rend.set_debug(0)
+            rend.set_debug(DYN)
             for rep in range(3):
                 a = rend.mlp_forward(X)
                 assert np.array_equal(a, ref), (n, rep, int((a != ref).sum()))
