@@ -46,9 +46,7 @@ struct nr_ctx {
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
     bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
-    bool no_dyn = false;     // nr_set_debug bit 12: k_mlp16 (bf16/fp16) without the dynamic tail
-    bool force_dyn = false;  // nr_set_debug bit 13: with it (an eighth) whatever NR_MLP16_DYN says
-    uint32_t *d_dyn = nullptr;  // its counters (MlpArgs::dyn_ctr), zero between launches
+    bool no_cuq = false;     // nr_set_debug bit 12: k_mlp16 (bf16/fp16) grid-stride, not the CU queue
     bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
                             // on the same packs
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
@@ -726,7 +724,7 @@ int nr_destroy(nr_ctx *c) {
     if (!(c->use_own && !c->own_stream)) (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_dyn); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
     dfree(c->d_frames); dfree(c->d_bout);
     if (c->h_frames) (void)hipHostFree(c->h_frames);
@@ -1220,19 +1218,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // 12 workgroups per CU by default: more than fit at once (3-5), so that workgroups start
         // staggered as earlier ones retire -- a grid of exactly the resident workgroups runs the
         // bf16 MLP 17 % slower (its waves stay in step: profiles/r3_mlp_bpc.txt)
-        // bf16/fp16: the last eighth of the chunks dealt dynamically (k_mlp16; counters zeroed once
-        // here, then by each launch's last wave)
+        // bf16/fp16: one 12-wave workgroup per CU with its own chunk queue (k_mlp16 CUQ)
         const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
         MlpArgs M = c->mlp16;
-        const int dyn = c->force_dyn ? 1 : NR_MLP16_DYN;
-        if (lowp && dyn > 0 && !c->no_dyn) {
-            if (!c->d_dyn) {
-                HIPCHK(c, hipMalloc(&c->d_dyn, 256));
-                HIPCHK(c, hipMemsetAsync(c->d_dyn, 0, 256, s));
-            }
-            M.dyn_ctr = c->d_dyn;
-            M.dyn_eighths = dyn;
-        }
+        M.lp_cuq = lowp && NR_MLP16_CUQ && !c->no_cuq ? num_cus(c->device) : 0;
         // (bf16/fp16 since round 4: the resident grid, 3 per CU -- with the pipelined stream it runs
         // 2^24 points in 0.218 against 0.232 ms at 12, profiles/r4_ab_dyn.txt)
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (lowp ? NR_MLP16_BPC_LP : 12);
@@ -1388,8 +1377,7 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
-    c->no_dyn = (flags >> 12) & 1;
-    c->force_dyn = (flags >> 13) & 1;
+    c->no_cuq = (flags >> 12) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;

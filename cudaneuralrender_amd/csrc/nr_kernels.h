@@ -6,12 +6,10 @@
 namespace nr {
 
 // Network packs resident in device memory, staged into LDS by every block.
-// bf16/fp16 k_mlp16: eighths of the chunks dealt dynamically at the end (MlpArgs::dyn_eighths;
-// 0 = grid-stride only: the default, since the claims' single counter serialises them at ~10 ns
-// each -- one eighth dynamic ran 0.359 instead of 0.218 ms on 2^24 points, profiles/r4_ab_dyn.txt)
-// and the grid the 16-bit MLP runs on (workgroups per CU; 3 = exactly the resident ones)
-#ifndef NR_MLP16_DYN
-#define NR_MLP16_DYN 0
+// bf16/fp16 k_mlp16: the per-CU chunk queue (MlpArgs::lp_cuq; 0 = off) and the grid of the
+// grid-stride form (workgroups per CU; 3 = exactly the resident ones)
+#ifndef NR_MLP16_CUQ
+#define NR_MLP16_CUQ 1
 #endif
 #ifndef NR_MLP16_BPC_LP
 #define NR_MLP16_BPC_LP 3
@@ -29,9 +27,8 @@ struct MlpArgs {
                             // waves whose inputs are all within F32_INPUT_BOUND
     int lp_stream;          // 16-bit MLP as the pipelined streams of nr_mlp16_asm.h (7 hidden
                             // layers); 0 (nr_set_debug bit 11): the builtin form, same values
-    uint32_t *dyn_ctr;      // bf16/fp16 k_mlp16: the dynamic tail's chunk counter ([0]) and
-                            // finished-wave counter ([32]), zero between launches
-    int dyn_eighths;        // eighths of the chunks dealt dynamically (0: every chunk grid-stride)
+    int lp_cuq;             // bf16/fp16 k_mlp16: > 0 = one 12-wave workgroup per CU dealing its
+                            // chunks through an LDS counter, on this many CUs; 0 = grid-stride
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,

@@ -735,10 +735,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_of(const void *p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
 // IN0: the network's inputs (3, or 4 with the frame): a template parameter, so that the load is
-// not behind a branch (whose join waited for it)
-template <int PREC, int IN0>
-__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
+// not behind a branch (whose join waited for it).  CUQ (bf16/fp16): one workgroup of 12 waves per
+// CU (3 per SIMD, every wave of the CU in it) dealing its share of the chunks through an LDS counter
+// (see the chunk loop); otherwise 4-wave workgroups dealing chunks grid-stride.
+template <int PREC, int IN0, bool CUQ = false>
+__global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                                     : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, int n) {
+    constexpr int WPG = CUQ ? 4 * NR_MLP16_WPS_LP : 4;  // waves per workgroup
+    __shared__ uint32_t cq[1];                           // CUQ: the workgroup's chunk counter
+    if (CUQ && threadIdx.x == 0) cq[0] = 0u;              // (stage16's barrier publishes it)
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     constexpr int in0 = IN0;
@@ -760,10 +765,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         }
     };
     auto store = [&](uint32_t i, float v) { __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), ry, i * 4u, 0, 0); };
-    // the wave's chunk index is uniform (SGPRs); launch_mlp16 launches 256-thread workgroups (blockDim,
+    // the wave's chunk index is uniform (SGPRs); launch_mlp16 launches WPG-wave workgroups (blockDim,
     // read from the dispatch packet by a vector load, would put the indices in VGPRs)
-    const int wave = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + (int)(threadIdx.x >> 6));
-    const int waves = __builtin_amdgcn_readfirstlane((int)gridDim.x * 4);
+    const int wave = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPG + (int)(threadIdx.x >> 6));
+    const int waves = __builtin_amdgcn_readfirstlane((int)gridDim.x * WPG);
     if constexpr (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16) {
         // 128 points per wave and chunk: point base + lane and base + 64 + lane; a last chunk of
         // at most 64 points takes the 64-point form
@@ -798,37 +803,44 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         unsigned long long st_mlp = 0;
         uint32_t st_n = 0;
 #endif
-        // Grid-stride chunks: a wave's chunks are wave, wave + waves, ... up to nstat; the last
-        // M.dyn_eighths / 8 of the chunks are then claimed one at a time from a counter, so that
-        // the waves finish together whatever their clocks and neighbours (grid-stride alone: the
-        // slowest wave's loop ran 13 % past the median, profiles/r4_mlp_stream_stamps.txt).  A
-        // claim is requested at the top of the chunk whose end needs it and read at that end, a
-        // whole MLP later.  (A queue dealing every chunk by atomics measured slower: the claims'
-        // round trips, ~2,500 cycles per chunk under load; profiles/r4_mlp_queue.txt.)
+        // Chunk dealing.  Grid-stride (4-wave workgroups, 3 per CU): a wave's chunks are wave, wave +
+        // waves, ...; but the oldest wave of each SIMD wins issue arbitration and runs its chunks at
+        // ~4,800 cycles against its neighbours' ~7,300, so it finishes its equal share at 2/3 of the
+        // loop and leaves the last third to two waves per SIMD (profiles/r4_mlp_stamps_hwid.txt).
+        // CUQ: the CU's 12 waves form one workgroup that owns a contiguous range of chunks and deals
+        // them one at a time through an LDS counter, so a faster wave simply takes more of them and
+        // the CU's waves finish within one chunk of each other.  (Dealing through global counters
+        // cost more than it balanced: one counter serialises its atomics at ~10 ns each, and even
+        // spread over 32 counters the claims' round trips stretched every chunk;
+        // profiles/r4_ab_dyn.txt.)  A claim is requested at the top of a chunk and read at its end.
         const uint32_t nch = (uint32_t)(nfull >> 7);
-        const uint32_t kst = M.dyn_eighths > 0 ? nch / 8u * (uint32_t)(8 - M.dyn_eighths) / (uint32_t)waves
-                                               : (nch + (uint32_t)waves - 1u) / (uint32_t)waves;
-        const int nstat = (int)min(nch, kst * (uint32_t)waves);
-        // the claim counter, lane 0 only (the others' offsets fall past the buffer and are dropped)
-        const auto rc = __builtin_amdgcn_make_buffer_rsrc(M.dyn_ctr, 0, 256, 0x00020000);
+        const int per = CUQ ? (int)((nch + gridDim.x - 1u) / gridDim.x) : 0;
+        const int lo = CUQ ? min((int)blockIdx.x * per, (int)nch) : 0, hi = CUQ ? min(lo + per, (int)nch) : 0;
         int gs = wave;
-        uint32_t claim_v = 0;   // the claim requested at this chunk's top (lane 0)
-        bool dyn_end = M.dyn_eighths <= 0;   // no claims (any more): a claim came back past the last chunk
+        uint32_t claim_v = 0;  // CUQ: the claim requested at this chunk's top (lane 0's value)
+        int claim_s = 0;       // ... moved to a scalar register before the MLP (no VGPR held across it)
+        // every lane adds 1 (a wave-uniform operand: hipcc's atomic optimizer makes it one ds_add of
+        // 64 by the first lane, where a lane-dependent operand became a 64-step scan loop), so a
+        // claim advances the counter by 64 and is its value >> 6
+        auto claim = [&]() {
+            if constexpr (CUQ) claim_v = atomicAdd(&cq[0], 1u);
+        };
+        auto settle = [&]() {
+            if constexpr (CUQ) claim_s = __builtin_amdgcn_readfirstlane((int)claim_v) >> 6;
+        };
         auto fixed = [&]() -> int {
-            if (gs < nstat) {
+            if constexpr (CUQ) {
+                const int c = lo + claim_s;
+                return c < hi ? c : -1;
+            } else {
                 const int c = gs;
                 gs += waves;
-                return c;
+                return c < (int)nch ? c : -1;
             }
-            if (dyn_end) return -1;
-            const int c = nstat + __builtin_amdgcn_readfirstlane((int)claim_v);
-            dyn_end = c >= (int)nch;
-            return dyn_end ? -1 : c;
         };
-        // the first two chunks: a wave with fewer than two static ones claims synchronously
         auto first = [&]() -> int {
-            if (gs >= nstat && !dyn_end)
-                claim_v = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 ? 0 : 0x7fffff00, 0, 0);
+            claim();
+            settle();
             return fixed();
         };
         int cur = first(), nxt = first();
@@ -851,10 +863,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             // everything in flight was issued a chunk ago: wait for it all here (free), so that
             // hipcc's scoreboard holds nothing older than this iteration's own requests
             __builtin_amdgcn_s_waitcnt(0x0f70);
-            // the claim the end of this chunk reads (when its static chunks are used up): issued by
-            // every lane, lanes 1-63 and chunks that need none at an offset the buffer drops
-            const bool need = gs >= nstat && !dyn_end;
-            claim_v = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 && need ? 0 : 0x7fffff00, 0, 0);
+            claim();  // the chunk after next (CUQ): settled below, consumed at this chunk's end
             const int base = cur * 128;
             const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
             const int nb = (nxt < 0 ? (int)nch : nxt) * 128;  // past the last chunk: zeros, unused
@@ -869,6 +878,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             const bool ok = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
                             __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
                             __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
+            settle();
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
                 mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
             else
@@ -887,17 +897,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
         while (cur >= 0) body();
         store((uint32_t)(pbase + lane), pv[0]);
         store((uint32_t)(pbase + 64 + lane), pv[1]);
-        // the dynamic tail's counters back to zero for the next launch: by the last wave to finish
-        // (every wave's claims have returned by now)
-        if (M.dyn_eighths > 0) {
-            __builtin_amdgcn_s_waitcnt(0);
-            const int done = __builtin_amdgcn_readfirstlane(
-                __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rc, lane == 0 ? 128 : 0x7fffff00, 0, 0));
-            if (done == waves - 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(0u, rc, lane == 0 ? 0 : 0x7fffff00, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(0u, rc, lane == 0 ? 128 : 0x7fffff00, 0, 0);
-            }
-        }
 #if NR_MLP16_STAMPS
         // diagnostic build: per wave {cycles in the loop, of them in the MLP calls, chunks} in Y
         const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -909,6 +908,10 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             // the loop's start and end on the chip's 100 MHz clock (low 24 bits), after the per-wave block
             Y[4 * waves + 2 * wave] = (float)(r0 & 0xffffffull);
             Y[4 * waves + 2 * wave + 1] = (float)(r1 & 0xffffffull);
+            // where the wave ran: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID, 16 bits each
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+            Y[6 * waves + 2 * wave] = (float)(hw & 0xffffu);
+            Y[6 * waves + 2 * wave + 1] = (float)(((hw >> 16) & 0xffu) | ((xcc & 0xfu) << 8));
         }
         return;
 #endif
@@ -984,12 +987,19 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         const int m = (int)std::min(SEG, n - p0);
         const float *x = X + p0 * M.in0;
         float *y = Y + p0;
-        // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane)
-        const long per_wg = lowp ? 512 : 256;
-        const int g = (int)std::max<long>(1, std::min<long>(grid, ((long)m + per_wg - 1) / per_wg));
-        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
+        // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane);
+        // bf16/fp16 with the CU queue (M.lp_cuq): one 12-wave workgroup per CU (grid = CUs)
+        const bool cuq = lowp && M.lp_cuq > 0;
+        const long per_wg = cuq ? 128l * 4 * NR_MLP16_WPS_LP : lowp ? 512 : 256;
+        const int g = (int)std::max<long>(1, std::min<long>(cuq ? M.lp_cuq : grid, ((long)m + per_wg - 1) / per_wg));
+        const int threads = cuq ? 64 * 4 * NR_MLP16_WPS_LP : 256;
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(threads), sm, st, M, x, y, m); };
         const bool four = M.in0 == 4;
-        if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
+        if (prec == NR_PRECISION_BF16 && cuq)
+            four ? go(k_mlp16<NR_PRECISION_BF16, 4, true>) : go(k_mlp16<NR_PRECISION_BF16, 3, true>);
+        else if (prec == NR_PRECISION_FP16 && cuq)
+            four ? go(k_mlp16<NR_PRECISION_FP16, 4, true>) : go(k_mlp16<NR_PRECISION_FP16, 3, true>);
+        else if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
         else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
         else if (prec == NR_PRECISION_FP32X3) four ? go(k_mlp16<NR_PRECISION_FP32X3, 4>) : go(k_mlp16<NR_PRECISION_FP32X3, 3>);
         else four ? go(k_mlp16<NR_PRECISION_FP32, 4>) : go(k_mlp16<NR_PRECISION_FP32, 3>);

@@ -127,26 +127,25 @@ def test_trace_stream_animation_frames_identical(rend, chrome):
         rend.set_static(nr.NR_COLOR_MATCAP, 3).set_precision("fp32")
 
 
-# ---- k_mlp16's dynamic tail (the last eighth of the chunks claimed from a counter)
+# ---- k_mlp16's per-CU chunk queue (one 12-wave workgroup per CU, chunks claimed through LDS)
 
-NO_DYN = 1 << 12
-DYN = 1 << 13
+NO_CUQ = 1 << 12
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_mlp_dynamic_tail_equals_grid_stride(rend, nets, prec):
-    """Every point evaluated exactly once whatever the split between grid-stride and claimed
-    chunks (all claimed below ~450 k points), the same values as the grid-stride launch (bit 12),
-    and the counters back at zero after every launch (repeated launches stay right)."""
+def test_mlp_cu_queue_equals_grid_stride(rend, nets, prec):
+    """Every point evaluated exactly once by the CU-queue launch (ragged sizes, fewer chunks than
+    CUs, a 4-input network below), the same values as the grid-stride launch (bit 12), and repeated
+    launches stay right."""
     dims, K, B = nets["car_1"]
     rend.load_mlp(dims, K, B).set_precision(prec)
     rng = np.random.default_rng(25)
     try:
         for n in (1, 129, 128 * 777 + 5, (1 << 18) + 77, (1 << 20) + 64, 3_000_001):
             X = rng.uniform(-1.2, 1.2, size=(n, 3)).astype(np.float32)
-            rend.set_debug(NO_DYN)
+            rend.set_debug(NO_CUQ)
             ref = rend.mlp_forward(X)
-            rend.set_debug(DYN)
+            rend.set_debug(0)
             for rep in range(3):
                 a = rend.mlp_forward(X)
                 assert np.array_equal(a, ref), (n, rep, int((a != ref).sum()))

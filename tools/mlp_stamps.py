@@ -19,9 +19,9 @@ r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
 for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
     r.set_precision(prec)
-    for debug in (4096, 4096 | 2048):
+    for debug in (0, 4096):
         r.set_debug(debug)
-        for bpc in (3, 12):
+        for bpc in (3,):
             r.set_occupancy(bpc)
             for _ in range(3):
                 Y.zero_()
@@ -52,6 +52,21 @@ for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
             by_xcd = {int(x): [round(float(np.median(t1[xcd == x])), 1), round(float(t1[xcd == x].max()), 1),
                                round(float(np.median(st2[xcd[: len(st2)] == x, 0] / np.maximum(st2[xcd[: len(st2)] == x, 2], 1))))]
                       for x in range(8)}
+            hw = Y[6 * waves: 8 * waves].view(waves, 2).cpu().numpy().astype(np.int64)
+            # HW_ID: wave 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13 (gfx9); XCC from XCC_ID
+            simd_key = ((hw[:, 1] >> 8) << 16) | (hw[:, 0] & 0xff30) | 0
+            cu_key = ((hw[:, 1] >> 8) << 16) | (hw[:, 0] & 0xff00)
+            _, inv, cnt = np.unique(simd_key, return_inverse=True, return_counts=True)
+            waves_on_simd = cnt[inv]
+            chunks = st2[:, 2] if len(st2) == waves else np.zeros(waves)
+            by_load = {int(k): {"waves": int((waves_on_simd == k).sum()),
+                                "end_us_median": round(float(np.median(t1[waves_on_simd == k])), 1),
+                                "chunks_median": float(np.median(chunks[waves_on_simd == k]))}
+                       for k in np.unique(waves_on_simd)}
+            simds = len(np.unique(simd_key))
+            cus = len(np.unique(cu_key))
+            if os.environ.get("STAMPS_NPZ"):
+                np.savez(os.environ["STAMPS_NPZ"] + f"_{prec}_{debug}_{bpc}.npz", st=st2, se=se, hw=hw)
             slot = (np.arange(waves) % 4)
             by_slot = {int(k): round(float(np.median(t1[slot == k])), 1) for k in range(4)}
             print(json.dumps({"precision": prec, "debug": debug, "bpc": bpc, "waves": int(len(st)),
@@ -63,5 +78,6 @@ for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
                               "loop_ms_median": round(float(np.median(st2[:, 3])) / 1e5, 4),
                               "start_us_max": round(float(t0.max()), 1), "end_us_p10_p50_p90_max":
                               [round(float(np.percentile(t1, q)), 1) for q in (10, 50, 90, 100)],
-                              "by_xcd_end_median_max_us_cycles_per_chunk": by_xcd, "by_wave_slot_end_us": by_slot}), flush=True)
+                              "by_xcd_end_median_max_us_cycles_per_chunk": by_xcd, "by_wave_slot_end_us": by_slot,
+                              "cus": cus, "simds": simds, "by_waves_on_simd": by_load}), flush=True)
 r.set_debug(0)
