@@ -46,7 +46,7 @@ struct nr_ctx {
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
     bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
-    bool no_cuq = false;     // nr_set_debug bit 12: k_mlp16 (bf16/fp16) grid-stride, not the CU queue
+    bool flip_cuq = false;   // nr_set_debug bit 12: k_mlp16 (bf16/fp16) in the other chunk-dealing form
     bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
                             // on the same packs
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
@@ -1218,12 +1218,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // 12 workgroups per CU by default: more than fit at once (3-5), so that workgroups start
         // staggered as earlier ones retire -- a grid of exactly the resident workgroups runs the
         // bf16 MLP 17 % slower (its waves stay in step: profiles/r3_mlp_bpc.txt)
-        // bf16/fp16: one 12-wave workgroup per CU with its own chunk queue (k_mlp16 CUQ)
+        // bf16/fp16: grid-stride, or one 12-wave workgroup per CU with its own chunk queue (CUQ)
         const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
         MlpArgs M = c->mlp16;
-        M.lp_cuq = lowp && NR_MLP16_CUQ && !c->no_cuq ? num_cus(c->device) : 0;
-        // (bf16/fp16 since round 4: the resident grid, 3 per CU -- with the pipelined stream it runs
-        // 2^24 points in 0.218 against 0.232 ms at 12, profiles/r4_ab_dyn.txt)
+        M.lp_cuq = lowp && ((NR_MLP16_CUQ != 0) != c->flip_cuq) ? num_cus(c->device) : 0;
         const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (lowp ? NR_MLP16_BPC_LP : 12);
         const int grid = num_cus(c->device) * bpc;
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
@@ -1377,7 +1375,7 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
-    c->no_cuq = (flags >> 12) & 1;
+    c->flip_cuq = (flags >> 12) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;

@@ -6,13 +6,16 @@
 namespace nr {
 
 // Network packs resident in device memory, staged into LDS by every block.
-// bf16/fp16 k_mlp16: the per-CU chunk queue (MlpArgs::lp_cuq; 0 = off) and the grid of the
-// grid-stride form (workgroups per CU; 3 = exactly the resident ones)
+// bf16/fp16 k_mlp16: the per-CU chunk queue by default (MlpArgs::lp_cuq; nr_set_debug bit 12
+// selects it at run time otherwise) and the grid of the grid-stride form (workgroups per CU).
+// Interleaved A/B on 2^24 points (tools/mlp_ab.py, profiles/r4_mlp_ab.txt): bf16 0.1951 (queue) /
+// 0.1989 (grid-stride, 3 per CU) / 0.1931 ms (12 per CU), fp16 0.2329 / 0.2369 / 0.2325 -- the
+// queue balances the waves (profiles/r4_mlp_stamps_hwid.txt) but the SIMD's chunk rate is the same
 #ifndef NR_MLP16_CUQ
-#define NR_MLP16_CUQ 1
+#define NR_MLP16_CUQ 0
 #endif
 #ifndef NR_MLP16_BPC_LP
-#define NR_MLP16_BPC_LP 3
+#define NR_MLP16_BPC_LP 12
 #endif
 
 struct MlpArgs {

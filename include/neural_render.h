@@ -228,9 +228,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected).  Bit 11 = the
  * bf16/fp16 MLP of 7-hidden-layer networks in its builtin-compiled form instead of the
  * software-pipelined instruction streams (nr_mlp16_asm.h; the same values, for A/B and parity).
- * Bit 12 = the bf16/fp16 nr_mlp_forward deals its 128-point chunks grid-stride over 4-wave
- * workgroups instead of through one 12-wave workgroup per CU with an LDS chunk queue (the same
- * values; A/B). */
+ * Bit 12 = the bf16/fp16 nr_mlp_forward deals its 128-point chunks through one 12-wave workgroup
+ * per CU with an LDS chunk queue instead of grid-stride over 4-wave workgroups (the same values;
+ * A/B, equal speed). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next

@@ -129,23 +129,23 @@ def test_trace_stream_animation_frames_identical(rend, chrome):
 
 # ---- k_mlp16's per-CU chunk queue (one 12-wave workgroup per CU, chunks claimed through LDS)
 
-NO_CUQ = 1 << 12
+CUQ = 1 << 12
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_mlp_cu_queue_equals_grid_stride(rend, nets, prec):
     """Every point evaluated exactly once by the CU-queue launch (ragged sizes, fewer chunks than
     CUs, a 4-input network below), the same values as the grid-stride launch (bit 12), and repeated
-    launches stay right."""
+    launches stay right.  (Bit 12 selects the queue.)"""
     dims, K, B = nets["car_1"]
     rend.load_mlp(dims, K, B).set_precision(prec)
     rng = np.random.default_rng(25)
     try:
         for n in (1, 129, 128 * 777 + 5, (1 << 18) + 77, (1 << 20) + 64, 3_000_001):
             X = rng.uniform(-1.2, 1.2, size=(n, 3)).astype(np.float32)
-            rend.set_debug(NO_CUQ)
-            ref = rend.mlp_forward(X)
             rend.set_debug(0)
+            ref = rend.mlp_forward(X)
+            rend.set_debug(CUQ)
             for rep in range(3):
                 a = rend.mlp_forward(X)
                 assert np.array_equal(a, ref), (n, rep, int((a != ref).sum()))

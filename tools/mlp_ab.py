@@ -4,8 +4,8 @@ drift over a run does not favour whichever form is measured first (a sequential 
 form ~10 % slower whatever it was).
 
     python tools/mlp_ab.py [--n 16777216] [--rounds 7] [--iters 10] [--precision bf16]
-Forms: "cuq" (library default: one 12-wave workgroup per CU, LDS chunk queue), "gs3" / "gs12"
-(grid-stride, 3 or 12 four-wave workgroups per CU: nr_set_debug bit 12 + nr_set_occupancy)."""
+Forms: "cuq" (one 12-wave workgroup per CU, LDS chunk queue: nr_set_debug bit 12), "gs3" / "gs12"
+(grid-stride, 3 or 12 four-wave workgroups per CU, nr_set_occupancy; gs12 is the library default)."""
 import argparse
 import json
 import os
@@ -29,7 +29,7 @@ X = torch.from_numpy(np.random.default_rng(0).uniform(-1, 1, size=(a.n, 3)).asty
 Y = torch.zeros(a.n, dtype=torch.float32, device="cuda")
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
-FORMS = {"cuq": (0, 0), "gs3": (4096, 3), "gs12": (4096, 12)}
+FORMS = {"cuq": (4096, 0), "gs3": (0, 3), "gs12": (0, 12)}
 for prec in a.precision.split(","):
     r.set_precision(prec)
     times = {f: [] for f in a.forms.split(",")}
