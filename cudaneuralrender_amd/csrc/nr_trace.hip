@@ -60,6 +60,19 @@ namespace nr {
 #define NR_NONMLP_PRIO 3
 #endif
 
+// bf16/fp16: issue priority NR_MLP_PRIO_LOWP inside the march MLP (the age-ordered arbitration
+// otherwise lets an older wave's scene/refill VALU cut into a younger wave's MFMA chain), and
+// NR_SHADE_PRIO_LOWP inside the shading pass's fp32 MLP, 0 elsewhere (0 = no change).  Alternating
+// A/B (tools/ab_trace_rounds.sh, profiles/r4_ab_prio.txt): march 2 -> C3 batch 1.370 / 1.389 vs
+// 1.379 / 1.405 ms, C5 1.410 / 1.417 vs 1.437 / 1.421; the shading priority, either alone or with
+// it, and 3 workgroups per CU were no better
+#ifndef NR_MLP_PRIO_LOWP
+#define NR_MLP_PRIO_LOWP 2
+#endif
+#ifndef NR_SHADE_PRIO_LOWP
+#define NR_SHADE_PRIO_LOWP 0
+#endif
+
 // Wave-private pools of pixel-queue positions reserved one atomic ahead (bf16/fp16
 // tracers only: their iterations are short, so the ~1 us reservation latency is a large
 // part of the refill; the fp32 tracer's MLP hides it and the pools only lengthen the
@@ -209,6 +222,8 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr int prec = PREC;
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
+    constexpr int MLP_PRIO = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16 ? NR_MLP_PRIO_LOWP : 0;
+    constexpr int SHADE_PRIO = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16 ? NR_SHADE_PRIO_LOWP : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     // rays generated in bulk through an LDS buffer (NR_DENSE_GEN): the reduced-precision tracers
     constexpr bool DENSE = NR_DENSE_GEN && (PREC != NR_PRECISION_FP32 || NR_DENSE_GEN_FP32) && !PROBE;
@@ -565,7 +580,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const F3 tp = mk3((qo == 0 || qo == 3) ? 1.0f : -1.0f, qo >= 2 ? 1.0f : -1.0f, (qo & 1) ? 1.0f : -1.0f);
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
+            if (SHADE_PRIO && !hold) set_priority(SHADE_PRIO);
             const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
+            if (SHADE_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
             const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
             if (k < nb && q4 == 0 && !T.itmap) {
@@ -613,9 +630,11 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         }
         // ---- MLP on every live point, then one sphere-trace step per ray
         if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
+        if (MLP_PRIO && !hold) set_priority(MLP_PRIO);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         if constexpr (timing) pt[3] += (drained && __popcll(lm) <= 4) ? 1 : 0;
         if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
+        if (MLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
