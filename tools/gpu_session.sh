@@ -17,7 +17,7 @@ for s in $STEPS; do
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$TAG.log 2>&1 ;;
     tests) timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=6 -v $PYTEST_EXTRA ${PYTEST_K:+-k "$PYTEST_K"} --timeout 300 --timeout-method thread > $O/gputests_$TAG.log 2>&1 ;;
     prof) timeout -k 10 900 bash tools/profile_round.sh $TAG > $O/profile_round_$TAG.log 2>&1 ;;
-    mlp) timeout -k 10 300 python -u tools/mlp_bench.py --n 16777216 --iters 10 --precision fp32,bf16,fp16,fp32x3 --bpc 8,12 > $O/mlp_$TAG.log 2>&1 ;;
+    mlp) timeout -k 10 300 python -u tools/mlp_bench.py --n 16777216 --iters 10 --precision fp32,bf16,fp16,fp32x3 --bpc 0 > $O/mlp_$TAG.log 2>&1 ;;
     cfg) timeout -k 10 400 python -u tools/config_bench.py --frames 5 > $O/cfg_$TAG.log 2>&1 ;;
     pmc_bf16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16_$TAG bf16 12 > $O/pmc_bf16_$TAG.txt 2>&1 ;;
     pmc_fp16) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_fp16_$TAG fp16 12 > $O/pmc_fp16_$TAG.txt 2>&1 ;;
