@@ -940,6 +940,8 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // (1024^2 x 32 frames 1.866 -> 1.825 ms/frame, one 8-way shard x 8 frames 0.367 ->
         // 0.334; profiles/r2_ab_experiments.txt (10)).  Debug bit 10: frame-major (A/B).
         T.interleave = !((c->debug >> 10) & 1);
+        // bf16/fp16: two ray groups per wave (k_trace2) or one (k_trace); debug bit 14: the other
+        T.two_groups = (NR_TRACE2 != 0) != (((c->debug >> 14) & 1) != 0);
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,

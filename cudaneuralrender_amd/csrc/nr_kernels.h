@@ -98,6 +98,13 @@ struct FrameArgs {
 };
 constexpr int NR_MAX_BATCH = 32;
 
+// batched bf16/fp16 launches on k_trace2 (two ray groups per wave) by default: 0 -- it measured
+// slower than k_trace (C3 1.47-1.50 vs 1.36-1.38 ms, C5 -13-15 %, profiles/r4_ab_trace2.txt);
+// nr_set_debug bit 14 selects the other tracer at run time
+#ifndef NR_TRACE2
+#define NR_TRACE2 0
+#endif
+
 struct TraceArgs {
     uint32_t *pix_ctr;          // 2^nq_shift pixel-queue shard counters, one per 128-byte line (stride 32)
     int nq_shift;
@@ -125,6 +132,7 @@ struct TraceArgs {
     int interleave;             // batched: 64-position queue chunks dealt to the frames in turn
                                 // (all frames progress together) instead of frame-major
     double inv_nframes;         // 1 / nframes for udiv_r
+    int two_groups;             // batched bf16/fp16: k_trace2 (two ray groups per wave) where it applies
 };
 
 int dense_lds_bytes(int in, int out);

@@ -230,7 +230,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * software-pipelined instruction streams (nr_mlp16_asm.h; the same values, for A/B and parity).
  * Bit 12 = the bf16/fp16 nr_mlp_forward deals its 128-point chunks through one 12-wave workgroup
  * per CU with an LDS chunk queue instead of grid-stride over 4-wave workgroups (the same values;
- * A/B, equal speed). */
+ * A/B, equal speed).  Bit 14 = batched bf16/fp16 launches on the tracer with two ray groups per wave
+ * (k_trace2: 128 rays per wave, one 128-point MLP per iteration) instead of k_trace (the same
+ * pixels; A/B -- it is slower). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next
