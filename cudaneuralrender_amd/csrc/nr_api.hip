@@ -42,6 +42,9 @@ struct nr_ctx {
     int precision = NR_PRECISION_FP32;
     float *d_pack16 = nullptr;
     uint16_t *d_lp16 = nullptr;
+    uint16_t *d_x3lp = nullptr;  // bf16/fp16: the fp32x3 pack for the normals (nr_set_debug bit 15)
+    float *d_x3fl = nullptr;
+    bool x3_normals = false;
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
@@ -170,7 +173,7 @@ int free_network(nr_ctx *c) {
     for (auto *p : c->d_W) (void)hipFree(p);
     for (auto *p : c->d_b) (void)hipFree(p);
     c->d_W.clear(); c->d_b.clear();
-    dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16);
+    dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16); dfree(c->d_x3lp); dfree(c->d_x3fl);
     c->fused = false;
     if (c->lgraph) { (void)hipGraphExecDestroy(c->lgraph); c->lgraph = nullptr; }
     c->lkey.clear();
@@ -214,7 +217,21 @@ int upload_lowp(nr_ctx *c) {
         return set_err(c, NR_E_INVALID, "low-precision pack failed");
     c->clamp_ok = clamp != 0;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp;
-    return upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
+    int rc = upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
+    if (rc != NR_OK) return rc;
+    // the fp32x3 pack beside it, for the normals (A/B: nr_set_debug bit 15), from global memory
+    dfree(c->d_x3lp); dfree(c->d_x3fl);
+    c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
+    std::vector<uint16_t> xa;
+    std::vector<float> xf;
+    int xok = 0;
+    if (NR_X3_NORMALS && pack_x3_32(c->dims, c->kernels, c->biases, xa, xf, &xok) && xok) {
+        MlpArgs X{};
+        if ((rc = upload_pack(c, xa, xf, c->d_x3lp, c->d_x3fl, X)) != NR_OK) return rc;
+        c->mlp16.x3lp = X.lp; c->mlp16.x3fl = X.lpf;
+        c->mlp16.x3n = c->x3_normals ? 1 : 0;
+    }
+    return NR_OK;
 }
 
 int set_network(nr_ctx *c, std::vector<int> dims, std::vector<std::vector<float>> K, std::vector<std::vector<float>> B) {
@@ -1377,6 +1394,8 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
+    c->x3_normals = (flags >> 15) & 1;
+    c->mlp16.x3n = c->x3_normals && c->mlp16.x3lp != nullptr;
     c->flip_cuq = (flags >> 12) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;

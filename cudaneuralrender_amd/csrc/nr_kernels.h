@@ -30,6 +30,9 @@ struct MlpArgs {
                             // waves whose inputs are all within F32_INPUT_BOUND
     int lp_stream;          // 16-bit MLP as the pipelined streams of nr_mlp16_asm.h (7 hidden
                             // layers); 0 (nr_set_debug bit 11): the builtin form, same values
+    const uint16_t *x3lp;   // bf16/fp16 tracers: the fp32x3 pack (global memory), for their normals
+    const float *x3fl;
+    int x3n;                // 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3, not fp32
     int lp_cuq;             // bf16/fp16 k_mlp16: > 0 = one 12-wave workgroup per CU dealing its
                             // chunks through an LDS counter, on this many CUs; 0 = grid-stride
 };
@@ -103,6 +106,12 @@ constexpr int NR_MAX_BATCH = 32;
 // nr_set_debug bit 14 selects the other tracer at run time
 #ifndef NR_TRACE2
 #define NR_TRACE2 0
+#endif
+// A/B (bf16/fp16 tracers): the shading pass's normals in fp32x3 -- 5x fewer MFMAs than the fp32
+// MLP, not bit-exact with it.  0 = off (the fp32 normals the emulation contract pins); 1 = selected
+// at run time by nr_set_debug bit 15; 2 = always, without the per-point fp32 fallback
+#ifndef NR_X3_NORMALS
+#define NR_X3_NORMALS 0
 #endif
 
 struct TraceArgs {

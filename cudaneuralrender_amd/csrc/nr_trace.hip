@@ -73,6 +73,7 @@ namespace nr {
 #define NR_SHADE_PRIO_LOWP 0
 #endif
 
+
 // Wave-private pools of pixel-queue positions reserved one atomic ahead (bf16/fp16
 // tracers only: their iterations are short, so the ~1 us reservation latency is a large
 // part of the refill; the fp32 tracer's MLP hides it and the pools only lengthen the
@@ -581,7 +582,19 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             if (SHADE_PRIO && !hold) set_priority(SHADE_PRIO);
-            const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
+            // (A/B, bf16/fp16: the normals in fp32x3 from the global-memory pack, M.x3n)
+            constexpr bool LOWP = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16;
+            // (the x3 pack's address made opaque here, so that its loop-invariant loads are not
+            // hoisted out of the shading loop into registers)
+            int zoff_x3 = 0;
+            if constexpr (LOWP && NR_X3_NORMALS) asm volatile("" : "+s"(zoff_x3));
+            const uint16_t *x3lp = M.x3lp + zoff_x3;
+            const float *x3fl = M.x3fl + zoff_x3;
+            const float sdf = LOWP && NR_X3_NORMALS == 2
+                                  ? mlp16_x3_split(M, x3lp, x3fl, fr_of(sfr), pq.x, pq.y, pq.z, smask)
+                              : LOWP && NR_X3_NORMALS && M.x3n
+                                  ? mlp16_x3(M, S.s32, x3lp, x3fl, fr_of(sfr), pq.x, pq.y, pq.z, smask, true)
+                                  : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             if (SHADE_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
             const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
