@@ -481,11 +481,15 @@ def test_mlp_stream_checker_rejects_hazards():
     spec = importlib.util.spec_from_file_location("gen_mlp_asm", gen)
     g = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(g)
-    st = g.build("bf16", True)
+    for nt in (4, 2):
+        _broken_streams(g, g.build("bf16", True, nt))
+
+
+def _broken_streams(g, st):
     ins = st.ins
 
     def broken(edit):
-        s2 = g.Stream()
+        s2 = g.Stream(st.nt)
         s2.ins = edit(list(ins))
         with pytest.raises(AssertionError):
             g.check(s2)
