@@ -29,7 +29,7 @@ EXPORTS = [
     "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
     "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
     "nr_h5_dims", "nr_h5_read_f32",
-    "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch",
+    "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch", "nr_pack_x3",
 ]
 
 
@@ -102,6 +102,8 @@ def lib():
         "nr_synchronize": (I, [P]),
         "nr_load_h5": (I, [P, ctypes.c_char_p]),
         "nr_load_mlp": (I, [P, I, IP, ctypes.POINTER(FP), ctypes.POINTER(FP)]),
+        "nr_pack_x3": (I, [I, IP, ctypes.POINTER(FP), ctypes.POINTER(FP), P, ctypes.c_long, P, ctypes.c_long,
+                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long), IP]),
         "nr_mlp_info": (I, [P, IP, IP, IP, IP]),
         "nr_set_precision": (I, [P, I]),
         "nr_set_view": (I, [P, FP, FP, I]),

@@ -42,9 +42,9 @@ struct nr_ctx {
     int precision = NR_PRECISION_FP32;
     float *d_pack16 = nullptr;
     uint16_t *d_lp16 = nullptr;
-    uint16_t *d_x3lp = nullptr;  // bf16/fp16: the fp32x3 pack for the normals (nr_set_debug bit 15)
+    uint16_t *d_x3lp = nullptr;  // bf16/fp16: the fp32x3 pack for the normals (MlpArgs::x3n)
     float *d_x3fl = nullptr;
-    bool x3_normals = false;
+    bool fp32_normals = false;   // nr_set_debug bit 15: the bf16/fp16 tracers' normals in fp32 (A/B)
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
@@ -200,6 +200,8 @@ int upload_lowp(nr_ctx *c) {
     dfree(c->d_lp16); dfree(c->d_lpf16);
     c->mlp16.lp = nullptr; c->mlp16.lpf = nullptr; c->mlp16.lp_bytes = 0; c->mlp16.lpf_bytes = 0;
     c->mlp16.lp_clamp = 0;
+    dfree(c->d_x3lp); dfree(c->d_x3fl);
+    c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
@@ -219,9 +221,8 @@ int upload_lowp(nr_ctx *c) {
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp;
     int rc = upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
     if (rc != NR_OK) return rc;
-    // the fp32x3 pack beside it, for the normals (A/B: nr_set_debug bit 15), from global memory
-    dfree(c->d_x3lp); dfree(c->d_x3fl);
-    c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
+    // the fp32x3 pack beside it, for the normals (read from global memory); a network whose
+    // pack is not valid keeps the fp32 normals
     std::vector<uint16_t> xa;
     std::vector<float> xf;
     int xok = 0;
@@ -229,7 +230,7 @@ int upload_lowp(nr_ctx *c) {
         MlpArgs X{};
         if ((rc = upload_pack(c, xa, xf, c->d_x3lp, c->d_x3fl, X)) != NR_OK) return rc;
         c->mlp16.x3lp = X.lp; c->mlp16.x3fl = X.lpf;
-        c->mlp16.x3n = c->x3_normals ? 1 : 0;
+        c->mlp16.x3n = c->fp32_normals ? 0 : 1;
     }
     return NR_OK;
 }
@@ -1208,6 +1209,30 @@ int nr_assemble_shards(nr_ctx *c, const uint32_t *src, size_t stride, uint32_t *
     return NR_OK;
 }
 
+int nr_pack_x3(int nlayers, const int *dims, const float *const *kernels, const float *const *biases, uint16_t *a,
+               long a_cap, float *f, long f_cap, long *a_len, long *f_len, int *ok) {
+    if (nlayers < 1 || !dims || !kernels || !biases || !a_len || !f_len || !ok)
+        return nr::report_error(NR_E_INVALID, "nr_pack_x3: bad arguments");
+    std::vector<int> d(dims, dims + nlayers + 1);
+    std::vector<std::vector<float>> K(nlayers), B(nlayers);
+    for (int l = 0; l < nlayers; ++l) {
+        if (!kernels[l] || !biases[l] || d[l] < 1 || d[l + 1] < 1)
+            return nr::report_error(NR_E_INVALID, "nr_pack_x3: layer %d", l);
+        K[l].assign(kernels[l], kernels[l] + (size_t)d[l] * d[l + 1]);
+        B[l].assign(biases[l], biases[l] + d[l + 1]);
+    }
+    std::vector<uint16_t> av;
+    std::vector<float> fv;
+    int k = 0;
+    if (!pack_x3_32(d, K, B, av, fv, &k)) return nr::report_error(NR_E_INVALID, "nr_pack_x3: not a fused shape");
+    *a_len = (long)av.size();
+    *f_len = (long)fv.size();
+    *ok = k;
+    if (a && a_cap >= (long)av.size()) std::memcpy(a, av.data(), av.size() * 2);
+    if (f && f_cap >= (long)fv.size()) std::memcpy(f, fv.data(), fv.size() * 4);
+    return NR_OK;
+}
+
 int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
     if (!c || (n > 0 && (!X || !Y)) || n < 0) return set_err(c, NR_E_INVALID, "nr_mlp_forward: bad arguments");
     if (c->dims.empty()) return set_err(c, NR_E_STATE, "nr_mlp_forward: no network loaded");
@@ -1394,8 +1419,8 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
-    c->x3_normals = (flags >> 15) & 1;
-    c->mlp16.x3n = c->x3_normals && c->mlp16.x3lp != nullptr;
+    c->fp32_normals = (flags >> 15) & 1;
+    c->mlp16.x3n = !c->fp32_normals && c->mlp16.x3lp != nullptr;
     c->flip_cuq = (flags >> 12) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;

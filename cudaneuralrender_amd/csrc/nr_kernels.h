@@ -32,7 +32,8 @@ struct MlpArgs {
                             // layers); 0 (nr_set_debug bit 11): the builtin form, same values
     const uint16_t *x3lp;   // bf16/fp16 tracers: the fp32x3 pack (global memory), for their normals
     const float *x3fl;
-    int x3n;                // 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3, not fp32
+    int x3n;                // bf16/fp16: 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3
+                            // (mlp16_x3_normal), 0 = in fp32
     int lp_cuq;             // bf16/fp16 k_mlp16: > 0 = one 12-wave workgroup per CU dealing its
                             // chunks through an LDS counter, on this many CUs; 0 = grid-stride
 };
@@ -107,11 +108,12 @@ constexpr int NR_MAX_BATCH = 32;
 #ifndef NR_TRACE2
 #define NR_TRACE2 0
 #endif
-// A/B (bf16/fp16 tracers): the shading pass's normals in fp32x3 -- 5x fewer MFMAs than the fp32
-// MLP, not bit-exact with it.  0 = off (the fp32 normals the emulation contract pins); 1 = selected
-// at run time by nr_set_debug bit 15; 2 = always, without the per-point fp32 fallback
+// bf16/fp16 tracers: the shading pass's normals (4 MLP evaluations per coloured ray) in fp32x3 --
+// 5x fewer MFMAs than the fp32 MLP (C3 -16 %, profiles/r4_x3_normals.txt), every point outside
+// the x3 pack's input bounds in fp32; the oracle restates both (nr_oracle.c mlp_point_gpu_x3).
+// 0 builds the fp32 normals only; nr_set_debug bit 15 selects them at run time (MlpArgs::x3n)
 #ifndef NR_X3_NORMALS
-#define NR_X3_NORMALS 0
+#define NR_X3_NORMALS 1
 #endif
 
 struct TraceArgs {

@@ -998,6 +998,32 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return in ? v3 : v32;
 }
 
+// The fp32 MLP as a call: the bf16/fp16 tracers' normals for points outside the x3 pack's input
+// bounds (never the bundled scenes' hit points).  Out of line, so that the fallback adds nothing
+// to the tracer's register demand at the shading site (inlined beside the split: 86 spilled VGPRs
+// in the bf16 tracer against 28).  s: LDS, read through the generic address space here.
+__device__ __noinline__ float mlp16_fp32_call(const float *s, int in0, int nh, float fr, float x, float y, float z,
+                                              uint32_t tmask, bool cl) {
+    return mlp16_fp32(s, in0, nh, fr, x, y, z, tmask, cl);
+}
+
+// bf16/fp16 tracers' normals (M.x3n): per point, the fp32x3 split for inputs within the x3 pack's
+// bounds, the fp32 MLP otherwise -- the same per-point rule as the fp32x3 precision (mlp16_x3), so
+// a normal never depends on the other rays of its wave.  Oracle: nr_oracle.c mlp_point_gpu_x3.
+__device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *s32, const uint16_t *lp,
+                                                 const float *fl, float fr, float x, float y, float z, uint32_t tmask) {
+    const bool in = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
+                    __builtin_fabsf(z) <= X3_INPUT_BOUND && (M.in0 != 4 || __builtin_fabsf(fr) <= X3_FRAME_BOUND);
+    float v = 0.0f;
+    if (__builtin_expect(__ballot(!in) != 0, 0))
+        v = mlp16_fp32_call(s32, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
+    if (__ballot(in) != 0) {
+        const float v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+        v = in ? v3 : v;
+    }
+    return v;
+}
+
 // The two-tile stream in the tracer's march (A/B knob, off): one wave alone runs the 64-point MLP
 // in 1,964 instead of 2,308 cycles, but the stream's 96 pinned registers push the tracer's live
 // state into scratch (bf16 batch: 8 -> 38 spilled VGPRs) and C3 runs 1.52 instead of 1.39 ms per

@@ -216,7 +216,8 @@ __device__ __forceinline__ void set_priority(int prio) {
 #ifndef NR_TRACE_BPC_X3
 #define NR_TRACE_BPC_X3 3
 #endif
-template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false>
+// NX3: the bf16/fp16 instances whose normals are fp32x3 (MlpArgs::x3n; mlp16_x3_normal).
+template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false>
 __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                   : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
                                   : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
@@ -582,18 +583,13 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             if (SHADE_PRIO && !hold) set_priority(SHADE_PRIO);
-            // (A/B, bf16/fp16: the normals in fp32x3 from the global-memory pack, M.x3n)
-            constexpr bool LOWP = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16;
-            // (the x3 pack's address made opaque here, so that its loop-invariant loads are not
-            // hoisted out of the shading loop into registers)
+            // NX3 (bf16/fp16, M.x3n): the normals in fp32x3 from the global-memory pack, whose
+            // address is made opaque here so that its loop-invariant loads are not hoisted out of
+            // the shading loop into registers held for the kernel's life
             int zoff_x3 = 0;
-            if constexpr (LOWP && NR_X3_NORMALS) asm volatile("" : "+s"(zoff_x3));
-            const uint16_t *x3lp = M.x3lp + zoff_x3;
-            const float *x3fl = M.x3fl + zoff_x3;
-            const float sdf = LOWP && NR_X3_NORMALS == 2
-                                  ? mlp16_x3_split(M, x3lp, x3fl, fr_of(sfr), pq.x, pq.y, pq.z, smask)
-                              : LOWP && NR_X3_NORMALS && M.x3n
-                                  ? mlp16_x3(M, S.s32, x3lp, x3fl, fr_of(sfr), pq.x, pq.y, pq.z, smask, true)
+            if constexpr (NX3) asm volatile("" : "+s"(zoff_x3));
+            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, M.x3lp + zoff_x3, M.x3fl + zoff_x3, fr_of(sfr), pq.x, pq.y,
+                                                    pq.z, smask)
                                   : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             if (SHADE_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
@@ -747,7 +743,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
 // Used for batched bf16/fp16 launches of 64 rays per wave (launch_trace; nr_set_debug bit 14:
 // k_trace).
 constexpr int STASH2 = 16 - 1 + 128;  // a shading pass leaves at most 15 rays; one iteration adds <= 128
-template <int PREC>
+template <int PREC, bool NX3 = false>
 __global__ __launch_bounds__(256, 3) void k_trace2(RenderArgs A, MlpArgs M, TraceArgs T) {
     static_assert(PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16, "reduced precision only");
     constexpr int RMIN = NR_REFILL_MIN_LOWP;
@@ -953,7 +949,11 @@ __global__ __launch_bounds__(256, 3) void k_trace2(RenderArgs A, MlpArgs M, Trac
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
             if (NR_SHADE_PRIO_LOWP) set_priority(NR_SHADE_PRIO_LOWP);
-            const float sdf = mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
+            int zoff_x3 = 0;  // (as k_trace's)
+            if constexpr (NX3) asm volatile("" : "+s"(zoff_x3));
+            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, M.x3lp + zoff_x3, M.x3fl + zoff_x3, fr_of(sfr), pq.x, pq.y,
+                                                    pq.z, smask)
+                                  : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             if (NR_SHADE_PRIO_LOWP) __builtin_amdgcn_s_setprio(0);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sf[sfr].zoff));
             const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
@@ -1393,6 +1393,31 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
     return hipSuccess;
 }
 
+// one k_trace instance: bf16/fp16 with fp32x3 normals when the network has the pack (M.x3n)
+template <int PREC, bool PROBE, bool STAMPS, bool BATCH>
+static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, int sm,
+                                 hipStream_t st) {
+    constexpr bool LOWP = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16;
+    if constexpr (LOWP && NR_X3_NORMALS && !PROBE) {
+        if (M.x3n) {
+            hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH>), dim3(grid), dim3(256), sm, st, A, M, T);
+    return hipGetLastError();
+}
+
+template <bool PROBE, bool STAMPS, bool BATCH>
+static hipError_t launch_trace_p(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, int sm,
+                                 hipStream_t st) {
+    if (prec == NR_PRECISION_BF16) return launch_trace_k<NR_PRECISION_BF16, PROBE, STAMPS, BATCH>(A, M, T, grid, sm, st);
+    if (prec == NR_PRECISION_FP16) return launch_trace_k<NR_PRECISION_FP16, PROBE, STAMPS, BATCH>(A, M, T, grid, sm, st);
+    if (prec == NR_PRECISION_FP32X3)
+        return launch_trace_k<NR_PRECISION_FP32X3, PROBE, STAMPS, BATCH>(A, M, T, grid, sm, st);
+    return launch_trace_k<NR_PRECISION_FP32, PROBE, STAMPS, BATCH>(A, M, T, grid, sm, st);
+}
+
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {
     const int sm = smem16_bytes(M, prec, true);
     // the batched bf16/fp16 tracer with two ray groups per wave: 64 rays per group, no diagnostics
@@ -1404,50 +1429,21 @@ hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return hipErrorInvalidDevice;
         const int g = std::max(1, std::min(grid, 3 * cus));
-        if (prec == NR_PRECISION_BF16)
+        const bool x3 = NR_X3_NORMALS && M.x3n;
+        if (prec == NR_PRECISION_BF16 && x3)
+            hipLaunchKernelGGL((k_trace2<NR_PRECISION_BF16, true>), dim3(g), dim3(256), sm, st, A, M, T);
+        else if (prec == NR_PRECISION_BF16)
             hipLaunchKernelGGL((k_trace2<NR_PRECISION_BF16>), dim3(g), dim3(256), sm, st, A, M, T);
+        else if (x3)
+            hipLaunchKernelGGL((k_trace2<NR_PRECISION_FP16, true>), dim3(g), dim3(256), sm, st, A, M, T);
         else
             hipLaunchKernelGGL((k_trace2<NR_PRECISION_FP16>), dim3(g), dim3(256), sm, st, A, M, T);
         return hipGetLastError();
     }
-    if (T.probe) {
-        if (prec == NR_PRECISION_BF16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP32X3)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-    } else if (T.nframes > 0) {
-        if (prec == NR_PRECISION_BF16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP32X3)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-    } else if (T.stamps) {
-        if (prec == NR_PRECISION_BF16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP32X3)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-    } else {
-        if (prec == NR_PRECISION_BF16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_BF16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP16)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP16, false>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_FP32X3)
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32X3, false>), dim3(grid), dim3(256), sm, st, A, M, T);
-        else
-            hipLaunchKernelGGL((k_trace<NR_PRECISION_FP32, false>), dim3(grid), dim3(256), sm, st, A, M, T);
-    }
-    return hipGetLastError();
+    if (T.probe) return launch_trace_p<true, false, false>(A, M, T, prec, grid, sm, st);
+    if (T.nframes > 0) return launch_trace_p<false, false, true>(A, M, T, prec, grid, sm, st);
+    if (T.stamps) return launch_trace_p<false, true, false>(A, M, T, prec, grid, sm, st);
+    return launch_trace_p<false, false, false>(A, M, T, prec, grid, sm, st);
 }
 
 }  // namespace nr

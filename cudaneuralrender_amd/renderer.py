@@ -81,6 +81,26 @@ def save_ppm(path, img):
     check(lib().nr_ppm_save(path.encode(), img.ctypes.data, img.shape[1], img.shape[0]))
 
 
+def pack_x3(dims, kernels, biases):
+    """The library's fp32x3 pack of a fused-shape network (nr_pack_x3; host only): (a_ops uint16,
+    floats float32, ok).  For the test oracle's emulation of the fp32x3 MLP (the bf16/fp16 tracers'
+    normals)."""
+    L = lib()
+    nl = len(kernels)
+    d = (ctypes.c_int * (nl + 1))(*dims)
+    ks = [np.ascontiguousarray(k, np.float32) for k in kernels]
+    bs = [np.ascontiguousarray(b, np.float32) for b in biases]
+    kp = (_FP * nl)(*[_fptr(k) for k in ks])
+    bp = (_FP * nl)(*[_fptr(b) for b in bs])
+    na, nf, ok = ctypes.c_long(0), ctypes.c_long(0), ctypes.c_int(0)
+    check(L.nr_pack_x3(nl, d, kp, bp, None, 0, None, 0, ctypes.byref(na), ctypes.byref(nf), ctypes.byref(ok)))
+    a = np.zeros(na.value, np.uint16)
+    f = np.zeros(nf.value, np.float32)
+    check(L.nr_pack_x3(nl, d, kp, bp, a.ctypes.data, na.value, f.ctypes.data, nf.value, ctypes.byref(na),
+                       ctypes.byref(nf), ctypes.byref(ok)))
+    return a, f, ok.value
+
+
 def shard_rows(H, band, nshards, shard):
     return lib().nr_shard_rows(H, band, nshards, shard)
 
@@ -352,7 +372,7 @@ class Renderer:
         return Z
 
 
-__all__ = ["Renderer", "camera", "read_keras_h5", "load_png", "save_png", "save_ppm", "shard_rows",
+__all__ = ["Renderer", "camera", "pack_x3", "read_keras_h5", "load_png", "save_png", "save_ppm", "shard_rows",
            "assemble_shards", "NR_COLOR_FACING", "NR_COLOR_MATCAP"]
 
 

@@ -101,6 +101,13 @@ int nr_load_h5(nr_ctx *ctx, const char *path);
  * matrix, biases[l] has dims[l+1] floats.  ReLU on all layers but the last. */
 int nr_load_mlp(nr_ctx *ctx, int nlayers, const int *dims,
                 const float *const *kernels, const float *const *biases);
+/* The fp32x3 pack of a [3|4, 32, ..., 32, 1] network (host only, no GPU): fp16 hi / residual
+ * operands a[*a_len] in the kernels' layout and the floats f[*f_len] (scaled biases, final layer,
+ * scales); *ok = 0 when the scales do not fit fp16 (the kernels then run fp32).  Copies only when
+ * the capacities suffice (call with a = f = NULL for the lengths).  For the test oracle's fp32x3
+ * emulation (the bf16/fp16 tracers' normals); not part of the reference's interface. */
+int nr_pack_x3(int nlayers, const int *dims, const float *const *kernels, const float *const *biases,
+               uint16_t *a, long a_cap, float *f, long f_cap, long *a_len, long *f_len, int *ok);
 int nr_mlp_info(const nr_ctx *ctx, int *nlayers, int *dims /* >= nlayers+1 or NULL */,
                 int *num_weight_params, int *num_bias_params);
 int nr_set_precision(nr_ctx *ctx, int precision);
@@ -232,7 +239,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * per CU with an LDS chunk queue instead of grid-stride over 4-wave workgroups (the same values;
  * A/B, equal speed).  Bit 14 = batched bf16/fp16 launches on the tracer with two ray groups per wave
  * (k_trace2: 128 rays per wave, one 128-point MLP per iteration) instead of k_trace (the same
- * pixels; A/B -- it is slower). */
+ * pixels; A/B -- it is slower).  Bit 15 = the bf16/fp16 tracers' normals (the four tetrahedron
+ * samples of every coloured ray) by the fp32 MLP instead of the fp32x3 split (A/B; the frames'
+ * march is the same, their shading moves by the two forms' rounding). */
 int nr_set_debug(nr_ctx *ctx, int flags);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next

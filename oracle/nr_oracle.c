@@ -220,6 +220,121 @@ static void mlp_point_gpu_lowp(const or_mlp *m, const or_lowp *q, const float *x
     y[0] = (half[0] + half[1]) + m->b[nl - 1][0];
 }
 
+/* ---- fp32x3 (NR_PRECISION_FP32X3's MLP, and the bf16/fp16 tracers' normals since round 4) ----
+ * The fp32x3 MLP as libnr computes it on the GPU (nr_mlp16.h mlp32_x3_nt), from the pack the caller
+ * hands over (the library's own nr_pack_x3 = nr_pack.cpp pack_x3_32: power-of-two scales from
+ * interval bounds, fp16 hi/residual weights in the kernel's operand layout), emulated for one point
+ * in the kernel's register layout: the point's two lanes (p, p + 32) hold accumulator registers
+ * acc[h][i] = row (i & 3) + 8 (i >> 2) + 4 h of the 32x32 MFMA's output.
+ *   layer 0   inputs scaled by 2^6, fp16 hi/lo split (RNE, residuals in f32), one K = 16 MFMA
+ *             (half 0 k = {xh, yh, zh, xl, yl, zl, fh, fl}, half 1 k = {xh, yh, zh, fh, 0 x4}),
+ *             the scaled bias as its accumulator;
+ *   hidden    each activation a split into ah = max(rtz_f16(a), +0) and al = clamp(rne_f16(a -
+ *             rtz_f16(a)), 0, 1); six K = 16 MFMAs: W_hi . al (k-step 0, 1), W_lo . ah (0, 1),
+ *             W_hi . ah (0, 1), onto the scaled bias;
+ *   final     per half an f32 fmaf chain over registers 0-15 of w_i max(acc_i, 0), then
+ *             (half 0 + half 1) + bias.
+ * Every MFMA is modelled as the exact sum of its 16 products and its accumulator, rounded once to
+ * f32 -- the model of mlp_point_gpu_lowp, an emulation for contracts, not a bit-exact restatement. */
+typedef struct { const uint16_t *a; const float *fl; int nh, in0; } or_x3;
+static or_x3 g_x3;   /* or_set_x3_pack: the normals of precision-1/2 renders (NULL a: fp32 normals) */
+
+static float f16_bits_to_f(uint16_t h)
+{
+    const int e = (h >> 10) & 31, m = h & 1023;
+    float v;
+    if (e == 0) v = ldexpf((float)m, -24);
+    else if (e == 31) v = m ? NAN : INFINITY;
+    else v = ldexpf((float)(m | 1024), e - 25);
+    return (h & 0x8000) ? -v : v;
+}
+
+/* binary16 rounded toward zero (cvt_pkrtz), widened; saturates at the largest finite value */
+static float rtz_fp16(float x)
+{
+    if (x == 0.0f || !isfinite(x)) return x;
+    float ax = fabsf(x);
+    if (ax >= 65504.0f) return x > 0 ? 65504.0f : -65504.0f;
+    int e; frexpf(ax, &e);
+    int shift = (e - 1 < -14) ? -14 : e - 1;
+    float q = ldexpf(1.0f, shift - 10);
+    float r = truncf(ax / q) * q;
+    return x < 0 ? -r : r;
+}
+
+static int x3_row(int h, int i) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+static void mlp_point_gpu_x3(const or_x3 *X, const float *xin, float *y)
+{
+    const int nh = X->nh, in0 = X->in0;
+    const float *F = X->fl + 32 + 32 * nh;
+    const float m1 = F[33], sx = F[34];
+    float acc[2][16], B[2][8];
+    {   /* layer 0 */
+        const float x = xin[0] * sx, yv = xin[1] * sx, z = xin[2] * sx, fr = in0 == 4 ? xin[3] : 0.0f;
+        const float xh = round_fp16(x), yh = round_fp16(yv), zh = round_fp16(z);
+        const float xl = round_fp16(x - xh), yl = round_fp16(yv - yh), zl = round_fp16(z - zh);
+        float fh = 0.0f, fl = 0.0f;
+        if (in0 == 4) { fh = round_fp16(fr); fl = round_fp16(fr - fh); }
+        const float b0[8] = { xh, yh, zh, xl, yl, zl, fh, fl }, b1[8] = { xh, yh, zh, fh, 0, 0, 0, 0 };
+        memcpy(B[0], b0, sizeof b0); memcpy(B[1], b1, sizeof b1);
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) {
+                const int m = x3_row(h, i);
+                double s = X->fl[h * 16 + i];
+                for (int hk = 0; hk < 2; ++hk)
+                    for (int k = 0; k < 8; ++k) s += (double)f16_bits_to_f(X->a[(m + 32 * hk) * 8 + k]) * B[hk][k];
+                acc[h][i] = (float)s;
+            }
+    }
+    for (int j = 0; j < nh; ++j) {   /* hidden */
+        float hi[2][2][8], lo[2][2][8];  /* [k-step][half][e] */
+        for (int st = 0; st < 2; ++st)
+            for (int h = 0; h < 2; ++h)
+                for (int e = 0; e < 8; ++e) {
+                    const float v = acc[h][8 * st + e], t = rtz_fp16(v);
+                    hi[st][h][e] = signbit(t) ? 0.0f : t;
+                    float l = round_fp16(fmaf(t, m1, v));
+                    lo[st][h][e] = l < 0.0f ? 0.0f : (l > 1.0f ? 1.0f : l);
+                }
+        const uint16_t *A = X->a + 512 + (size_t)j * 2048;
+        float nxt[2][16];
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) {
+                const int m = x3_row(h, i);
+                float d = X->fl[32 + 32 * j + h * 16 + i];
+                /* (A operand part, k-step, activation part): W_hi.al, W_lo.ah, W_hi.ah, k-steps 0 then 1 */
+                static const int order[6][3] = { { 0, 0, 1 }, { 0, 1, 1 }, { 1, 0, 0 }, { 1, 1, 0 }, { 0, 0, 0 }, { 0, 1, 0 } };
+                for (int o = 0; o < 6; ++o) {
+                    const int part = order[o][0], st = order[o][1], act_lo = order[o][2];
+                    double s = d;
+                    for (int hk = 0; hk < 2; ++hk)
+                        for (int e = 0; e < 8; ++e) {
+                            const float w = f16_bits_to_f(A[part * 1024 + st * 512 + (m + 32 * hk) * 8 + e]);
+                            s += (double)w * (act_lo ? lo[st][hk][e] : hi[st][hk][e]);
+                        }
+                    d = (float)s;
+                }
+                nxt[h][i] = d;
+            }
+        memcpy(acc, nxt, sizeof acc);
+    }
+    float zt[2];
+    for (int h = 0; h < 2; ++h) {   /* final: f32 fmaf chain per half */
+        float a = 0.0f;
+        for (int i = 0; i < 16; ++i) a = fmaf(F[16 * h + i], fmaxf(acc[h][i], 0.0f), a);
+        zt[h] = a;
+    }
+    y[0] = (zt[0] + zt[1]) + F[32];
+}
+
+/* the x3 pack for the normals of precision-1/2 renders (the bf16/fp16 tracers' since round 4);
+ * a = NULL: fp32 normals.  Not thread-safe against concurrent renders. */
+void or_set_x3_pack(const uint16_t *a, const float *fl, int nh, int in0)
+{
+    g_x3.a = a; g_x3.fl = fl; g_x3.nh = nh; g_x3.in0 = in0;
+}
+
 /* precision 3: the network evaluated exactly (fp64 products and sums, ReLU in fp64), the output
  * rounded once to f32 -- the arithmetic-independent value every fp32-class evaluation order
  * (CUTLASS's unpinned SIMT order, the fp32x3 matrix-core split, ...) approximates.  Used to
@@ -249,6 +364,15 @@ static void mlp_point(const or_mlp *m, const or_lowp *q, const float *x, float *
     if (precision == 3) {
         mlp_point_f64(m, x, y);
         return;
+    }
+    if (precision == 4) {   /* fp32x3 (g_x3), the fp32 MLP outside the pack's input bounds */
+        const int in0 = m->dims[0];
+        if (g_x3.a && fabsf(x[0]) <= 4.0f && fabsf(x[1]) <= 4.0f && fabsf(x[2]) <= 4.0f &&
+            (in0 == 3 || fabsf(x[3]) <= 1024.0f)) {
+            mlp_point_gpu_x3(&g_x3, x, y);
+            return;
+        }
+        precision = 0;
     }
     if (precision != 0 && q) {
         mlp_point_gpu_lowp(m, q, x, y);
@@ -731,7 +855,7 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
             } else {
                 for (unsigned q = 0; q < mv; ++q) {
                     size_t o = bi + (size_t)q * ni;
-                    bprec[idmap[i] + q] = 0;
+                    bprec[idmap[i] + q] = (precision == 1 || precision == 2) && g_x3.a ? 4 : 0;
                     batch[o] = points[3 * i] + TET[3 * q] * NORMAL_EPSILON;
                     batch[o + 1] = points[3 * i + 1] + TET[3 * q + 1] * NORMAL_EPSILON;
                     batch[o + 2] = points[3 * i + 2] + TET[3 * q + 2] * NORMAL_EPSILON;

@@ -51,6 +51,8 @@ def lib():
         L.or_batch_cylinders.argtypes = [P, P, ctypes.c_long, P, P]
         L.or_batch_intersect.restype = None
         L.or_batch_intersect.argtypes = [P, P, ctypes.c_long, ctypes.c_float, P, P]
+        L.or_set_x3_pack.restype = None
+        L.or_set_x3_pack.argtypes = [P, P, I, I]
         _lib = L
     return _lib
 
@@ -69,14 +71,28 @@ def pack_params(kernels, biases):
 
 
 class OracleNet:
-    def __init__(self, kernels, biases):
+    def __init__(self, kernels, biases, x3_pack=None):
+        """x3_pack = (a_ops uint16, floats float32) from the library's nr_pack_x3 (the fp32x3 pack):
+        precision 4 evaluates with the fp32x3 emulation (nr_oracle.c mlp_point_gpu_x3), and
+        precision-1/2 renders take their normals from it, as the bf16/fp16 tracers do.  None: fp32
+        normals."""
         self.dims, self.params = pack_params(kernels, biases)
         self.nlayers = len(kernels)
+        self.x3 = None
+        if x3_pack is not None:
+            self.x3 = (np.ascontiguousarray(x3_pack[0], np.uint16), np.ascontiguousarray(x3_pack[1], np.float32))
+
+    def _x3_on(self):
+        if self.x3 is None:
+            lib().or_set_x3_pack(None, None, 0, 0)
+        else:
+            lib().or_set_x3_pack(self.x3[0].ctypes.data, self.x3[1].ctypes.data, self.nlayers - 2, int(self.dims[0]))
 
     def forward(self, X, precision=0, nthreads=0):
         X = np.ascontiguousarray(X, np.float32)
         n = X.shape[0]
         Y = np.zeros((n, int(self.dims[-1])), np.float32)
+        self._x3_on()
         rc = lib().or_mlp_forward(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, X.ctypes.data, n,
                                   X.shape[1], Y.ctypes.data, precision, nthreads)
         assert rc == 0, rc
@@ -85,7 +101,8 @@ class OracleNet:
     def render(self, W, H, inv_view, normal, frame=0, color_type=0, num_inputs=3, scene=0, matcap=None,
                max_steps=6000, nthreads=0, precision=0, rows=None):
         """precision 1/2: the GPU's bf16/fp16 MLP arithmetic (nr_oracle.c mlp_point_gpu_lowp) for
-        the marching points, fp32 normals.  rows=(y0, y1): render only those rows of the frame."""
+        the marching points; the normals in fp32x3 when the net holds an x3 pack (as the bf16/fp16
+        tracers compute them), else fp32.  rows=(y0, y1): render only those rows of the frame."""
         y0, y1 = rows if rows is not None else (0, H)
         out = np.zeros((y1 - y0, W), np.uint32)
         stats = np.zeros(5, np.int64)
@@ -96,6 +113,7 @@ class OracleNet:
             mp, mw, mh = mc.ctypes.data, mc.shape[1], mc.shape[0]
         else:
             mc, mp, mw, mh = None, None, 0, 0
+        self._x3_on()
         rc = lib().or_render_ex(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, iv.ctypes.data,
                                 nm.ctypes.data, frame, color_type, num_inputs, scene, mp, mw, mh, W, H, max_steps,
                                 out.ctypes.data, stats.ctypes.data, nthreads, precision, y0, y1)

@@ -49,6 +49,28 @@ def record():
 
 
 @pytest.mark.parametrize("geom", GEOMS)
+def test_x3_mlp_matches_oracle_emulation(golden, nets, geom, record):
+    """The oracle's fp32x3 emulation (nr_oracle.c mlp_point_gpu_x3, from the library's own pack)
+    against the GPU's fp32x3 MLP on the KAT points and a uniform cloud: the emulation that pins the
+    bf16/fp16 tracers' normals.  Each MFMA is modelled as an exact sum rounded once, so agreement
+    is near-total, not guaranteed bit-exact."""
+    dims, K, B = nets[geom]
+    rng = np.random.default_rng(11)
+    X = np.concatenate([golden["kat"]["X"], rng.uniform(-1.2, 1.2, size=(8192, 3)).astype(np.float32)])
+    with nr.Renderer(0) as r:
+        y = r.load_h5(nr.geometry_path(geom)).set_precision("fp32x3").mlp_forward(X)[:, 0]
+    pack = nr.pack_x3(dims, K, B)
+    assert pack[2]
+    e = oracle.OracleNet(K, B, x3_pack=pack[:2]).forward(X, precision=4)[:, 0]
+    d = np.abs(y.astype(np.float64) - e)
+    same = float((y == e).mean())
+    record.append({"test": "x3_emulation", "geometry": geom, "identical": same, "max_abs": float(d.max()),
+                   "ulp_1_or_less": float((np.abs(y.view(np.int32).astype(np.int64) - e.view(np.int32)) <= 1).mean())})
+    assert same >= 0.99, (same, d.max())
+    assert d.max() <= 1e-6, (same, d.max())
+
+
+@pytest.mark.parametrize("geom", GEOMS)
 def test_x3_mlp_kat(golden, nets, geom):
     dims, K, B = nets[geom]
     X = golden["kat"]["X"]

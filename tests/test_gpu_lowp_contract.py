@@ -59,7 +59,10 @@ def contract(name, geom, size, steps, prec, rows, chrome, record):
         r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
         img, st = r.render(size, size, steps)
     gpu = img[rows[0]:rows[1]]
-    net = oracle.OracleNet(K, B)
+    # the emulation computes the normals as the bf16/fp16 tracers do: fp32x3 from the library's pack
+    # (nr_pack_x3; nr_oracle.c mlp_point_gpu_x3), fp32 where the pack is not valid
+    pack = nr.pack_x3(dims, K, B)
+    net = oracle.OracleNet(K, B, x3_pack=pack[:2] if pack[2] else None)
     kw = dict(color_type=1, matcap=chrome, max_steps=steps, nthreads=16, rows=rows)
     emu, _ = net.render(size, size, iv, nm, precision=PREC[prec], **kw)
     f32, _ = net.render(size, size, iv, nm, precision=0, **kw)
