@@ -23,6 +23,11 @@ REF_CAMERAS = {"plane_1": (-18.8021, 149.7984, 2.2702), "car_1": (80.0, 140.0, 3
 
 
 @pytest.fixture(scope="session")
+def golden_dir():
+    return os.path.join(REPO, "tests", "golden")
+
+
+@pytest.fixture(scope="session")
 def golden():
     import numpy as np
     d = os.path.join(REPO, "tests", "golden")

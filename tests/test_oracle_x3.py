@@ -3,6 +3,8 @@ normals since round 4 (nr_mlp16.h mlp16_x3_normal), checked on the CPU against t
 network evaluated exactly (tests/golden/mlp_kat.npz, fp64 over the h5py weights) and against the
 oracle's own fp32 path where the split does not apply.  The pack is the library's (nr_pack_x3),
 computed on the host -- no GPU call."""
+import os
+
 import numpy as np
 import pytest
 
@@ -71,3 +73,50 @@ def test_x3_normals_in_the_bf16_render(nets):
     assert sa["ray_steps"] == sb["ray_steps"] and sa["rays_hit"] == sb["rays_hit"] > 100
     assert sa["shade_evals"] == sb["shade_evals"]
     assert not np.array_equal(ia, ib)
+
+
+@pytest.mark.parametrize("geom", ["plane_1", "car_1"])
+def test_mfma_fast_path_equals_generic(nets, geom):
+    """The restatement's decoded-operand fast path (nr_oracle.c mfma_fast) and its generic form
+    (mfma_sum_e on doubles) are the same arithmetic: bf16, fp16 and fp32x3 outputs bit for bit."""
+    dims, K, B = nets[geom]
+    X = np.random.default_rng(5).uniform(-1.3, 1.3, size=(384, 3)).astype(np.float32)
+    net = oracle.OracleNet(K, B, x3_pack=nr.pack_x3(dims, K, B)[:2])
+    try:
+        fast = {p: net.forward(X, precision=p, nthreads=1) for p in (1, 2, 4)}
+        oracle.set_mfma_model(3, -1)
+        slow = {p: net.forward(X, precision=p, nthreads=1) for p in (1, 2, 4)}
+    finally:
+        oracle.set_mfma_model(3, 26)
+    for p in (1, 2, 4):
+        np.testing.assert_array_equal(fast[p], slow[p])
+
+
+def _from16(u, prec):
+    if prec == "f16":
+        return u.view(np.float16).astype(np.float64)
+    return (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("prec,emin", [("f16", -14), ("bf16", -126)])
+def test_mfma_model_against_measured_hardware(golden_dir, prec, emin):
+    """The oracle's model of one v_mfma_f32_32x32x16_{f16,bf16} output (nr_oracle.c mfma_sum_e,
+    both its generic and fast forms) against outputs measured on gfx950 (tests/golden/mfma_*.npz,
+    made by tests/golden/make_mfma_golden.py from tools/mfma_cases.py and tools/mfma_model.py
+    runs): the 167 hand-built dot products and 10,240 random outputs over five kinds of operand
+    distribution, every one bit for bit."""
+    z = np.load(os.path.join(golden_dir, f"mfma_{prec}.npz"))
+    for i in range(len(z["hand_d"])):
+        for fast in (0, 1):
+            r = oracle.mfma_sum(z["hand_c"][i], z["hand_a"][i], z["hand_b"][i], emin, fast)
+            assert np.float32(r) == z["hand_d"][i], (i, fast, r, float(z["hand_d"][i]))
+    for kind in ("cancel", "generic", "residual", "tiny", "x3_like"):
+        A, B = _from16(z[kind + "_A"], prec), _from16(z[kind + "_B"], prec)
+        C, D = z[kind + "_C"], z[kind + "_D"]
+        bad = 0
+        for m in range(A.shape[0]):
+            for r in range(32):
+                for c in range(32):
+                    v = oracle.mfma_sum(C[m, r, c], A[m, r], B[m, :, c], emin, (r + c) & 1)
+                    bad += np.float32(v) != D[m, r, c]
+        assert bad == 0, (kind, bad)

@@ -37,6 +37,12 @@ def to16(x, prec):
     return u, (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
 
 
+def from16(u, prec):
+    if prec == "f16":
+        return u.view(np.float16).astype(np.float64)
+    return (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
 def cases(n, prec, rng):
     """n matrices of each kind: (kind, A[n,32,16], B[n,16,32], C[n,32,32]) as float64"""
     out = []
@@ -128,24 +134,39 @@ def main():
     ap.add_argument("--prec", default="f16")
     ap.add_argument("--n", type=int, default=24)
     ap.add_argument("--sample", type=int, default=3000, help="outputs per kind scored against the models")
+    ap.add_argument("--save", default="", help="write the cases and the hardware's outputs to this .npz and stop")
+    ap.add_argument("--load", default="", help="score the models on a --save file (no GPU)")
     a = ap.parse_args()
     if a.build:
         build()
         return
     rng = np.random.default_rng(5)
-    L = ctypes.CDLL(SO)
-    L.mfma_probe.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int]
     res = {}
     MS = models()
-    for kind, A, B, C in cases(a.n, a.prec, rng):
-        Au, Af = to16(A, a.prec)
-        Bu, Bf = to16(B, a.prec)
-        Cf = C.astype(np.float32)
-        D = np.zeros((a.n, 32, 32), np.float32)
-        Au, Bu = np.ascontiguousarray(Au), np.ascontiguousarray(Bu)
-        rc = L.mfma_probe(Au.ctypes.data, Bu.ctypes.data, Cf.ctypes.data, D.ctypes.data, a.n, int(a.prec == "bf16"))
-        assert rc == 0
-        idx = rng.choice(a.n * 1024, size=min(a.sample, a.n * 1024), replace=False)
+    if a.load:
+        z = np.load(a.load)
+        kinds = sorted({k.rsplit("_", 1)[0] for k in z.files})
+        runs = [(k, z[k + "_A"], z[k + "_B"], z[k + "_C"], z[k + "_D"]) for k in kinds]
+    else:
+        L = ctypes.CDLL(SO)
+        L.mfma_probe.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int, ctypes.c_int]
+        runs = []
+        for kind, A, B, C in cases(a.n, a.prec, rng):
+            Au, _ = to16(A, a.prec)
+            Bu, _ = to16(B, a.prec)
+            Cf = C.astype(np.float32)
+            D = np.zeros((a.n, 32, 32), np.float32)
+            Au, Bu = np.ascontiguousarray(Au), np.ascontiguousarray(Bu)
+            rc = L.mfma_probe(Au.ctypes.data, Bu.ctypes.data, Cf.ctypes.data, D.ctypes.data, a.n, int(a.prec == "bf16"))
+            assert rc == 0
+            runs.append((kind, Au, Bu, Cf, D))
+    for kind, Au, Bu, Cf, D in runs:
+        Af, Bf = from16(Au, a.prec), from16(Bu, a.prec)
+        if a.save:
+            res[kind] = (Au, Bu, Cf, D)
+            continue
+        n = len(D)
+        idx = rng.choice(n * 1024, size=min(a.sample, n * 1024), replace=False)
         score = {}
         for ftz in (False,):
             tiny = 2.0 ** -14 if a.prec == "f16" else 2.0 ** -126
@@ -163,6 +184,9 @@ def main():
         best = sorted(score.items(), key=lambda kv: -kv[1])[:6]
         res[kind] = score
         print(json.dumps({"prec": a.prec, "kind": kind, "best": best}), flush=True)
+    if a.save:
+        np.savez_compressed(a.save, **{f"{k}_{n}": v for k, t in res.items() for n, v in zip("ABCD", t)})
+        return
     tot = {k: float(np.mean([res[kind][k] for kind in res])) for k in next(iter(res.values()))}
     print(json.dumps({"prec": a.prec, "overall_best": sorted(tot.items(), key=lambda kv: -kv[1])[:8]}), flush=True)
 
