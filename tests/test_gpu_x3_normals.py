@@ -64,10 +64,12 @@ def test_x3_normals_against_their_emulation(rend, nets, chrome, prec):
     assert np.array_equal(b, eb), compare_frames(b, eb)
 
 
-def _net4(seed=6):
+def _net4(seed=41, scale=1.4):
+    """a [4, 32 x 8, 1] network whose x3 and fp32 normals give visibly different texels (checked
+    on the oracle: 3,982 of 4,096 pixels at 64^2)"""
     rng = np.random.default_rng(seed)
     dims = [4] + [32] * 8 + [1]
-    K = [(rng.standard_normal((dims[i], dims[i + 1])) * (1.0 / np.sqrt(dims[i]))).astype(np.float32) for i in range(9)]
+    K = [(rng.standard_normal((dims[i], dims[i + 1])) * (scale / np.sqrt(dims[i]))).astype(np.float32) for i in range(9)]
     B = [(rng.standard_normal(dims[i + 1]) * 0.05).astype(np.float32) for i in range(9)]
     B[-1][0] = 0.3
     return dims, K, B
