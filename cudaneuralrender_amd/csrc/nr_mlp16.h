@@ -998,6 +998,10 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return in ? v3 : v32;
 }
 
+// the tracers' x3 normals on 64 points: 2 = one two-tile pass, 1 = two one-tile passes (A/B)
+#ifndef NR_X3_NORMAL_TILES
+#define NR_X3_NORMAL_TILES 2
+#endif
 // The fp32 MLP as a call: the bf16/fp16 tracers' normals for points outside the x3 pack's input
 // bounds (never the bundled scenes' hit points).  Out of line, so that the fallback adds nothing
 // to the tracer's register demand at the shading site (inlined beside the split: 86 spilled VGPRs
@@ -1018,7 +1022,22 @@ __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *
     if (__builtin_expect(__ballot(!in) != 0, 0))
         v = mlp16_fp32_call(s32, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
     if (__ballot(in) != 0) {
-        const float v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+        float v3;
+        if (NR_X3_NORMAL_TILES == 1 && (tmask & 0xcu)) {
+            // two one-tile passes instead of one two-tile pass (fewer live registers at the
+            // shading site): the second on tile 1's points moved to lanes 0-31
+            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, 0x3u);
+            float a0, a1, b0, b1, c0, c1, d0, d1;
+            half_views(x, a0, a1);
+            half_views(y, b0, b1);
+            half_views(z, c0, c1);
+            half_views(fr, d0, d1);
+            const bool lo = lane_id() < 32;
+            const float v1 = mlp16_x3_split(M, lp, fl, lo ? d1 : d0, lo ? a1 : a0, lo ? b1 : b0, lo ? c1 : c0, 0x3u);
+            v3 = lo ? v3 : v1;
+        } else {
+            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+        }
         v = in ? v3 : v;
     }
     return v;
