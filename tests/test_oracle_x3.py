@@ -120,3 +120,29 @@ def test_mfma_model_against_measured_hardware(golden_dir, prec, emin):
                     v = oracle.mfma_sum(C[m, r, c], A[m, r], B[m, :, c], emin, (r + c) & 1)
                     bad += np.float32(v) != D[m, r, c]
         assert bad == 0, (kind, bad)
+
+
+def test_pack_x3_rejects_non_fused_shapes():
+    """nr_pack_x3 takes [3|4, 32, ..., 32, 1] only; any other shape is NR_E_INVALID with a message
+    (the library's error convention), not a crash."""
+    rng = np.random.default_rng(2)
+    dims = [3, 48, 1]
+    K = [rng.standard_normal((3, 48)).astype(np.float32), rng.standard_normal((48, 1)).astype(np.float32)]
+    B = [np.zeros(48, np.float32), np.zeros(1, np.float32)]
+    with pytest.raises(Exception) as e:
+        nr.pack_x3(dims, K, B)
+    assert "fused" in str(e.value) or "invalid" in str(e.value).lower()
+
+
+def test_x3_oracle_pack_lifecycle(nets):
+    """The oracle's decoded x3 operands follow the pack it is handed: two networks alternating in
+    one process give each its own values (or_set_x3_pack re-decodes on every call)."""
+    X = np.random.default_rng(8).uniform(-1, 1, size=(64, 3)).astype(np.float32)
+    outs = {}
+    for g in ("plane_1", "car_1", "plane_1"):
+        dims, K, B = nets[g]
+        y = oracle.OracleNet(K, B, x3_pack=nr.pack_x3(dims, K, B)[:2]).forward(X, precision=4)
+        if g in outs:
+            np.testing.assert_array_equal(outs[g], y)
+        outs[g] = y
+    assert not np.array_equal(outs["plane_1"], outs["car_1"])
