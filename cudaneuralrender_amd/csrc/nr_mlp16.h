@@ -998,9 +998,10 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return in ? v3 : v32;
 }
 
-// the tracers' x3 normals on 64 points: 2 = one two-tile pass, 1 = two one-tile passes (A/B)
+// the tracers' x3 normals on 64 points: 1 = two one-tile passes (28 -> 9 spilled VGPRs in the bf16
+// batch tracer; C3 -1.7 %, profiles/r4_ab_x3_tiles.txt), 2 = one two-tile pass
 #ifndef NR_X3_NORMAL_TILES
-#define NR_X3_NORMAL_TILES 2
+#define NR_X3_NORMAL_TILES 1
 #endif
 // The fp32 MLP as a call: the bf16/fp16 tracers' normals for points outside the x3 pack's input
 // bounds (never the bundled scenes' hit points).  Out of line, so that the fallback adds nothing
