@@ -49,7 +49,6 @@ struct nr_ctx {
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
     bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
-    bool flip_cuq = false;   // nr_set_debug bit 12: k_mlp16 (bf16/fp16) in the other chunk-dealing form
     bool no_clamp = false;  // nr_set_debug bit 9: bf16 ReLU by v_pk_max_i16, fp32 by add + max,
                             // on the same packs
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
@@ -226,7 +225,7 @@ int upload_lowp(nr_ctx *c) {
     std::vector<uint16_t> xa;
     std::vector<float> xf;
     int xok = 0;
-    if (NR_X3_NORMALS && pack_x3_32(c->dims, c->kernels, c->biases, xa, xf, &xok) && xok) {
+    if (pack_x3_32(c->dims, c->kernels, c->biases, xa, xf, &xok) && xok) {
         MlpArgs X{};
         if ((rc = upload_pack(c, xa, xf, c->d_x3lp, c->d_x3fl, X)) != NR_OK) return rc;
         c->mlp16.x3lp = X.lp; c->mlp16.x3fl = X.lpf;
@@ -958,8 +957,6 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // (1024^2 x 32 frames 1.866 -> 1.825 ms/frame, one 8-way shard x 8 frames 0.367 ->
         // 0.334; profiles/r2_ab_experiments.txt (10)).  Debug bit 10: frame-major (A/B).
         T.interleave = !((c->debug >> 10) & 1);
-        // bf16/fp16: two ray groups per wave (k_trace2) or one (k_trace); debug bit 14: the other
-        T.two_groups = (NR_TRACE2 != 0) != (((c->debug >> 14) & 1) != 0);
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,
@@ -1262,11 +1259,10 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         // 12 workgroups per CU by default: more than fit at once (3-5), so that workgroups start
         // staggered as earlier ones retire -- a grid of exactly the resident workgroups runs the
         // bf16 MLP 17 % slower (its waves stay in step: profiles/r3_mlp_bpc.txt)
-        // bf16/fp16: grid-stride, or one 12-wave workgroup per CU with its own chunk queue (CUQ)
-        const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
-        MlpArgs M = c->mlp16;
-        M.lp_cuq = lowp && ((NR_MLP16_CUQ != 0) != c->flip_cuq) ? num_cus(c->device) : 0;
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : (lowp ? NR_MLP16_BPC_LP : 12);
+        // (a per-CU LDS chunk queue balanced the SIMD's waves but left the kernel time unchanged,
+        // round 4: profiles/r4_mlp_ab.txt)
+        const MlpArgs M = c->mlp16;
+        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : 12;
         const int grid = num_cus(c->device) * bpc;
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, c->precision, dX, dY, (int)n,
@@ -1421,7 +1417,6 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->no_stream = (flags >> 11) & 1;
     c->fp32_normals = (flags >> 15) & 1;
     c->mlp16.x3n = !c->fp32_normals && c->mlp16.x3lp != nullptr;
-    c->flip_cuq = (flags >> 12) & 1;
     c->mlp16.lp_stream = !c->no_stream;
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp && c->mlp16.lp != nullptr;
     c->mlp16.f32_clamp = c->f32_clamp_ok && !c->no_clamp;

@@ -190,9 +190,6 @@ __device__ __forceinline__ float sqrt_rn_normal(float x) {
     return rp > 0.0f ? sp : r;
 }
 
-#ifndef NR_SCENE_SCREEN
-#define NR_SCENE_SCREEN 1
-#endif
 __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // The reference walks cP through the 3x3 grid with f64 updates (cP.y -= 0.6,
     // cP.z += ..., per row cP.y += 0.4 and cP.x = p.x + 0.5, per sphere cP.x -= 0.4);
@@ -217,7 +214,7 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // wave of scattered rays nearly every sphere has some lane near it, so skipping the
     // square roots of far spheres behind a branch cost more than it saved
     // (tools/scene_bench.hip).
-    float q[9], d[9];
+    float q[9];
 #pragma unroll
     for (int row = 0; row < 3; ++row)
 #pragma unroll
@@ -228,7 +225,6 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
     // ones), the short sequence gives the same bits as sqrtf.
     const float lo = fmaxf(zz, fmaxf(fminf(fminf(xx[0], xx[1]), xx[2]), fminf(fminf(yy[0], yy[1]), yy[2])));
     const float hi = (fmaxf(fmaxf(xx[0], xx[1]), xx[2]) + fmaxf(fmaxf(yy[0], yy[1]), yy[2])) + zz;
-#if NR_SCENE_SCREEN
     // Screening (round 3): smoothUnion(s, d, k) with d - s >= k is fmaf(d, 0, s) -- it does not
     // depend on d's value, only on that test (and on d's sign when s is +-0, where the test
     // already makes d >= k > 0).  The running union never exceeds the surface value nsdf
@@ -265,19 +261,6 @@ __device__ float many_sphere(F3 p, float nsdf, double zoff) {  // :176-196
 #pragma unroll
     for (int i = 0; i < 9; ++i) s = smooth_union(s, sqrtf(q[i]) - 0.1f, 0.01f);
     return s;
-#else
-    if (__ballot(!(lo >= 0x1p-96f && hi <= 0x1.fffffep127f)) == 0) {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) d[i] = sqrt_rn_normal(q[i]) - 0.1f;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 9; ++i) d[i] = sqrtf(q[i]) - 0.1f;
-    }
-    float s = nsdf;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) s = smooth_union(s, d[i], 0.01f);
-    return s;
-#endif
 }
 
 // manySphere(p, nSDF, false) (:176-196): the 9 spheres smooth-subtracted from the surface,

@@ -32,8 +32,7 @@ __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__re
 // The same for the 16-bit MLP on 128 points (k_mlp16's form, mlp32_lowp_128; 7 hidden layers):
 // PART 0 = the whole evaluation (the stream if M.lp_stream, else the builtin form), PART 1 = the
 // pipelined stream alone (nr_mlp16_asm.h), its outputs fed back as its inputs; and on the
-// tracer's 64 points (mlp16_lowp, one point per lane): PART 2 = two 32-point tiles (the two-tile
-// stream if M.lp_stream), PART 3 = one.  Y[0] = shader cycles per evaluation.
+// tracer's 64 points (mlp16_lowp, one point per lane): PART 2 = two 32-point tiles, PART 3 = one.  Y[0] = shader cycles per evaluation.
 template <int PREC, int PART>
 __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
                                                        int reps) {
@@ -57,8 +56,7 @@ __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *_
             const float xr[2] = {x[0] + v[0] * 1e-30f, x[1] + v[1] * 1e-30f};
             mlp32_lowp_128<PREC, 7, CL>(slp, sfl, M.in0, 7, fr, xr, y, z, v, M.lp_stream != 0);
         } else if constexpr (PART >= 2) {
-            v[0] = mlp16_lowp<PREC>(slp, sfl, M.in0, 7, 0.0f, x[0] + v[0] * 1e-30f, y[0], z[0], PART == 2 ? 0xfu : 0x3u, CL,
-                                    M.lp_stream != 0);
+            v[0] = mlp16_lowp<PREC>(slp, sfl, M.in0, 7, 0.0f, x[0] + v[0] * 1e-30f, y[0], z[0], PART == 2 ? 0xfu : 0x3u, CL);
         } else {
             mlp7_x4_stream<PREC, CL>(slp, sfl, kk);
             for (int t = 0; t < 4; ++t) kk[t][0] = kk[t][1] & 0x3f003f00u;

@@ -6,18 +6,6 @@
 namespace nr {
 
 // Network packs resident in device memory, staged into LDS by every block.
-// bf16/fp16 k_mlp16: the per-CU chunk queue by default (MlpArgs::lp_cuq; nr_set_debug bit 12
-// selects it at run time otherwise) and the grid of the grid-stride form (workgroups per CU).
-// Interleaved A/B on 2^24 points (tools/mlp_ab.py, profiles/r4_mlp_ab.txt): bf16 0.1951 (queue) /
-// 0.1989 (grid-stride, 3 per CU) / 0.1931 ms (12 per CU), fp16 0.2329 / 0.2369 / 0.2325 -- the
-// queue balances the waves (profiles/r4_mlp_stamps_hwid.txt) but the SIMD's chunk rate is the same
-#ifndef NR_MLP16_CUQ
-#define NR_MLP16_CUQ 0
-#endif
-#ifndef NR_MLP16_BPC_LP
-#define NR_MLP16_BPC_LP 12
-#endif
-
 struct MlpArgs {
     const float *pk;        // fp32 pack (nr_internal.h PK_*; 32- or 16-wide layout)
     const uint16_t *lp;     // bf16/fp16 A operands (precision != fp32)
@@ -34,8 +22,6 @@ struct MlpArgs {
     const float *x3fl;
     int x3n;                // bf16/fp16: 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3
                             // (mlp16_x3_normal), 0 = in fp32
-    int lp_cuq;             // bf16/fp16 k_mlp16: > 0 = one 12-wave workgroup per CU dealing its
-                            // chunks through an LDS counter, on this many CUs; 0 = grid-stride
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
@@ -102,19 +88,6 @@ struct FrameArgs {
 };
 constexpr int NR_MAX_BATCH = 32;
 
-// batched bf16/fp16 launches on k_trace2 (two ray groups per wave) by default: 0 -- it measured
-// slower than k_trace (C3 1.47-1.50 vs 1.36-1.38 ms, C5 -13-15 %, profiles/r4_ab_trace2.txt);
-// nr_set_debug bit 14 selects the other tracer at run time
-#ifndef NR_TRACE2
-#define NR_TRACE2 0
-#endif
-// bf16/fp16 tracers: the shading pass's normals (4 MLP evaluations per coloured ray) in fp32x3 --
-// 5x fewer MFMAs than the fp32 MLP (C3 -16 %, profiles/r4_x3_normals.txt), every point outside
-// the x3 pack's input bounds in fp32; the oracle restates both (nr_oracle.c mlp_point_gpu_x3).
-// 0 builds the fp32 normals only; nr_set_debug bit 15 selects them at run time (MlpArgs::x3n)
-#ifndef NR_X3_NORMALS
-#define NR_X3_NORMALS 1
-#endif
 
 struct TraceArgs {
     uint32_t *pix_ctr;          // 2^nq_shift pixel-queue shard counters, one per 128-byte line (stride 32)
@@ -143,7 +116,6 @@ struct TraceArgs {
     int interleave;             // batched: 64-position queue chunks dealt to the frames in turn
                                 // (all frames progress together) instead of frame-major
     double inv_nframes;         // 1 / nframes for udiv_r
-    int two_groups;             // batched bf16/fp16: k_trace2 (two ray groups per wave) where it applies
 };
 
 int dense_lds_bytes(int in, int out);

@@ -535,7 +535,7 @@ __global__ __launch_bounds__(256) void k_shade16(RenderArgs A, MlpArgs M, QueueA
         const long rem = n_s - off;  // rays; 4 per 16-point tile
         const uint32_t tmask = rem >= 16 ? 0xfu : (1u << ((rem + 3) >> 2)) - 1u;
         // bf16/fp16: the normals in fp32x3 (M.x3n), as the persistent tracer's
-        const float sdf = NR_X3_NORMALS && M.x3n
+        const float sdf = M.x3n
                               ? mlp16_x3_normal(M, S.s32, M.x3lp, M.x3fl, F[f].frame_f, pq.x, pq.y, pq.z, tmask)
                               : mlp16_fp32(M, S.s32, F[f].frame_f, pq.x, pq.y, pq.z, tmask);
         shade_rays(A, F[f].normal, F[f].out, F[f].zoff, live, sp, sd, tag & WF_PMASK, sdf);

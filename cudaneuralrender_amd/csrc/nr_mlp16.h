@@ -65,7 +65,7 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
                                                float y, float z) {
     auto relu = [](float v) { return CL ? __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f) : fmaxf(v, 0.0f); };
     // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
-    const int lane = lane_id(), g = lane >> 4, j = lane & 15;
+    const int lane = lane_id(), g = lane >> 4;
     float a[NT][8];
     f32x4 c[NT][2];
     // layer 0 on the matrix core too: K = in0 padded to 4 (weight 0 for the pad, whose
@@ -202,10 +202,6 @@ __device__ __forceinline__ bool inputs_in_bound_f32(float x, float y, float z, f
     return __ballot(!ok) == 0;
 }
 
-// fp32 ReLU form: NR_F32_CLAMP 0 builds the add + max form only (A/B)
-#ifndef NR_F32_CLAMP
-#define NR_F32_CLAMP 1
-#endif
 // cl (wave-uniform): the pack is scaled (MlpArgs::f32_clamp) and the inputs are within the
 // bound -- the clamped form on the active tiles; otherwise (never on the bundled networks'
 // rays) the add + max form on all four tiles, which keeps one extra copy of the MLP code
@@ -213,17 +209,13 @@ __device__ __forceinline__ bool inputs_in_bound_f32(float x, float y, float z, f
 __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
                                             float z, uint32_t tmask, bool cl) {
     const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
-    if (NR_F32_CLAMP && cl) {
+    if (cl) {
         if (nt >= 4) return mlp16_fp32_nt<4, 0, true>(s, in0, nh, fr, x, y, z);
         if (nt == 3) return mlp16_fp32_nt<3, 0, true>(s, in0, nh, fr, x, y, z);
         if (nt == 2) return mlp16_fp32_nt<2, 0, true>(s, in0, nh, fr, x, y, z);
         return mlp16_fp32_nt<1, 0, true>(s, in0, nh, fr, x, y, z);
     }
-    if (NR_F32_CLAMP) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
-    if (nt >= 4) return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
-    if (nt == 3) return mlp16_fp32_nt<3>(s, in0, nh, fr, x, y, z);
-    if (nt == 2) return mlp16_fp32_nt<2>(s, in0, nh, fr, x, y, z);
-    return mlp16_fp32_nt<1>(s, in0, nh, fr, x, y, z);
+    return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
 }
 __device__ __forceinline__ float mlp16_fp32(const MlpArgs &M, const float *s, float fr, float x, float y, float z,
                                             uint32_t tmask) {
@@ -338,28 +330,13 @@ __device__ __forceinline__ void relu_clamp_bf16_x2(const f32x16 &c, const f32x16
           "v"(d[8]), "v"(d[9]), "v"(d[10]), "v"(d[11]), "v"(d[12]), "v"(d[13]), "v"(d[14]), "v"(d[15]),
           "v"(t0), "v"(t1));
 }
-// A/B (NR_LP_CVT_PRIO): raise the wave's issue priority over its conversion block, so that a
-// wave leaves the VALU-only phase sooner and the matrix pipe idles less while every wave of the
-// SIMD converts
-#ifndef NR_LP_CVT_PRIO
-#define NR_LP_CVT_PRIO 0
-#endif
-#if NR_LP_CVT_PRIO
-#define NR_CVT_PRIO_ON "s_setprio " NR_STR(NR_LP_CVT_PRIO) "\n"
-#define NR_CVT_PRIO_OFF "s_setprio 0\n"
-#define NR_STR2(x) #x
-#define NR_STR(x) NR_STR2(x)
-#else
-#define NR_CVT_PRIO_ON ""
-#define NR_CVT_PRIO_OFF ""
-#endif
 // four tiles (the 128-point MLP): one block, so that no MFMA of the next layer can be scheduled
 // between the conversions of two tile pairs while the pair not yet converted is read
 __device__ __forceinline__ void relu_clamp_bf16_x4(const f32x16 &c0, const f32x16 &c1, const f32x16 &c2, const f32x16 &c3,
                                                    u32x4 (&k)[4][2]) {
     const uint32_t t0 = __float_as_uint(c0[0]) & 1u, t1 = __float_as_uint(c1[0]) & 1u;  // the touches
     const uint32_t t2 = __float_as_uint(c2[0]) & 1u, t3 = __float_as_uint(c3[0]) & 1u;
-    asm(NR_CVT_PRIO_ON NR_CVC(0, 32, 33) NR_CVC(1, 34, 35) NR_CVC(2, 36, 37) NR_CVC(3, 38, 39)
+    asm(NR_CVC(0, 32, 33) NR_CVC(1, 34, 35) NR_CVC(2, 36, 37) NR_CVC(3, 38, 39)
          NR_CVC(4, 40, 41) NR_CVC(5, 42, 43) NR_CVC(6, 44, 45) NR_CVC(7, 46, 47)
          NR_CVC(8, 48, 49) NR_CVC(9, 50, 51) NR_CVC(10, 52, 53) NR_CVC(11, 54, 55)
          NR_CVC(12, 56, 57) NR_CVC(13, 58, 59) NR_CVC(14, 60, 61) NR_CVC(15, 62, 63)
@@ -367,7 +344,7 @@ __device__ __forceinline__ void relu_clamp_bf16_x4(const f32x16 &c0, const f32x1
          NR_CVC(20, 72, 73) NR_CVC(21, 74, 75) NR_CVC(22, 76, 77) NR_CVC(23, 78, 79)
          NR_CVC(24, 80, 81) NR_CVC(25, 82, 83) NR_CVC(26, 84, 85) NR_CVC(27, 86, 87)
          NR_CVC(28, 88, 89) NR_CVC(29, 90, 91) NR_CVC(30, 92, 93) NR_CVC(31, 94, 95)
-        NR_CVT_PRIO_OFF "s_nop 1"
+        "s_nop 1"
         : "=&v"(k[0][0][0]), "=&v"(k[0][0][1]), "=&v"(k[0][0][2]), "=&v"(k[0][0][3]),
           "=&v"(k[0][1][0]), "=&v"(k[0][1][1]), "=&v"(k[0][1][2]), "=&v"(k[0][1][3]),
           "=&v"(k[1][0][0]), "=&v"(k[1][0][1]), "=&v"(k[1][0][2]), "=&v"(k[1][0][3]),
@@ -478,91 +455,26 @@ __device__ __forceinline__ float hi16f(uint32_t p) {
     else return (float)__builtin_bit_cast(_Float16, (uint16_t)(p >> 16));
 }
 
-// The pipelined streams (nr_mlp16_asm.h, tools/gen_mlp_asm.py) for the 7-hidden-layer networks:
-// 1 = on (MlpArgs::lp_stream, cleared by nr_set_debug bit 11, selects them at run time), 0 = never
-#ifndef NR_LP_STREAM
-#define NR_LP_STREAM 1
-#endif
+// The pipelined stream (nr_mlp16_asm.h, tools/gen_mlp_asm.py) of the 7-hidden-layer networks runs
+// k_mlp16's 128-point form (MlpArgs::lp_stream; nr_set_debug bit 11 selects the builtin form).
 
 // LDS byte address of a pointer into shared memory
 __device__ __forceinline__ uint32_t lds_addr(const void *p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
 }
 
-// Input layer + 7 hidden layers + the final layer's operand conversion of two 32-point tiles (the
-// tracer's 64 points) as one software-pipelined stream: tile 1's conversions beside tile 0's MFMAs,
-// the next layer's tile 0 beside tile 1's, every layer's operands read one layer ahead into the
-// idle one of two register buffers (nr_mlp16_asm.h NR_HID7X2_*).  In: k[t][0] = tile t's
-// input-layer B operand; out: k[t][s] = the final layer's ReLU'd B operands -- relu_pack_tiles'
-// values after hidden_layers, bit for bit.  Registers pinned to v0-v95.
-template <int PREC, bool CL>
-__device__ __forceinline__ void mlp7_x2_stream(const uint16_t *__restrict__ lp, const float *__restrict__ fl,
-                                               u32x4 (&k)[2][2]) {
-    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
-    const int lane = lane_id();
-    const uint32_t va = lds_addr(lp) + 16u * (uint32_t)lane, vb = lds_addr(fl) + 64u * (uint32_t)(lane >> 5);
-    f32x16 c0, c1, bb0, bb1;
-    u32x8 ab0, ab1;
-#define NR_STREAM_OPERANDS                                                                                          \
-    : "+{v[32:35]}"(k[0][0]), "=&{v[36:39]}"(k[0][1]), "+{v[40:43]}"(k[1][0]), "=&{v[44:47]}"(k[1][1]),            \
-      "=&{v[0:15]}"(c0), "=&{v[16:31]}"(c1), "=&{v[48:55]}"(ab0), "=&{v[56:63]}"(ab1), "=&{v[64:79]}"(bb0),         \
-      "=&{v[80:95]}"(bb1)                                                                                          \
-    : [va] "v"(va), [vb] "v"(vb)                                                                                   \
-    : "memory"
-    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_HID7X2_BF16_CLAMP NR_STREAM_OPERANDS);
-    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_HID7X2_BF16_MAX NR_STREAM_OPERANDS);
-    else asm volatile(NR_HID7X2_F16_MAX NR_STREAM_OPERANDS);
-#undef NR_STREAM_OPERANDS
-}
-
 // CL: ReLU by the conversion's clamp (bf16 with the clamped pack, inputs within
 // LP_INPUT_BOUND -- the caller checks); otherwise cvt + v_pk_max_i16 (any pack, any input).
-// stream: two tiles of a 7-hidden-layer network take the pipelined stream (mlp7_x2_stream).
+// (The tracer's 64 points as a two-tile pipelined stream: one wave alone 2,308 -> 1,964 cycles,
+// but the stream's 96 pinned registers spilled the tracer's state, C3 +9 %; round 4,
+// profiles/r4_ab_stream.txt.)
 template <int PREC, int NT, int NH, bool CL>
 __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                               int nh_rt, float fr, float x, float y, float z, bool stream = false) {
+                                               int nh_rt, float fr, float x, float y, float z) {
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
     f32x16 acc[NT];
-    if constexpr (NR_LP_STREAM && NT == 2 && NH == 7) {
-        if (stream) {
-            // the input layer's B operands exactly as below, then the stream, then the final layer
-            const uint32_t p0 = cvt2<PREC>(x, y);
-            const float dx = x - lo16f<PREC>(p0), dy = y - hi16f<PREC>(p0);
-            const uint32_t q = cvt2<PREC>(z, dx);
-            const uint32_t r = cvt2<PREC>(dy, z - lo16f<PREC>(q));
-            uint32_t f = 0;
-            if (in0 == 4) {
-                const uint32_t f0 = cvt2<PREC>(fr, 0.0f);
-                f = cvt2<PREC>(fr, fr - lo16f<PREC>(f0));
-            }
-            const uint32_t qf = (q & 0xffffu) | (f << 16);
-            const auto w0 = __builtin_amdgcn_permlane32_swap(p0, p0, false, false);
-            const auto w1 = __builtin_amdgcn_permlane32_swap(q, qf, false, false);
-            const auto w2 = __builtin_amdgcn_permlane32_swap(r, 0u, false, false);
-            const auto w3 = __builtin_amdgcn_permlane32_swap(f, 0u, false, false);
-            u32x4 kk[2][2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) kk[t][0] = (u32x4){w0[t], w1[t], w2[t], w3[t]};
-            mlp7_x2_stream<PREC, CL>(lp, fl, kk);
-            const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(7));
-            const u32x4 wf[2] = {F4[h], F4[2 + h]};
-            const float bf = fl[32 + 32 * 7];
-            float zt[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                float a = 0.0f;
-#pragma unroll
-                for (int st = 0; st < 2; ++st)
-#pragma unroll
-                    for (int qq = 0; qq < 4; ++qq) a = dot2<PREC>(kk[t][st][qq], wf[st][qq], a);
-                zt[t] = a;
-            }
-            const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[0]), __float_as_uint(zt[1]), false, false);
-            return (__uint_as_float(rr[0]) + __uint_as_float(rr[1])) + bf;
-        }
-    }
     {
         // B operand of tile t, lanes 0-31 (k 0-7) of point l: {xh, yh | zh, xl | yl, zl | fh, fl};
         // lanes 32-63 (k 8-15) of point l - 32: {xh, yh | zh, fh | 0 | 0}.  Each lane splits
@@ -635,13 +547,6 @@ __device__ __forceinline__ float mlp32_lowp_nt(const uint16_t *__restrict__ lp, 
 // per 64 points against 30 MFMAs: 196 LDS-array cycles per 960 MFMA cycles on each of the 4
 // SIMDs, MI355X_MICROARCH.md section LDS), and a layer's four independent MFMA chains give the
 // wave's own conversions more to overlap with.
-#ifndef NR_LP_FINAL_MFMA
-#define NR_LP_FINAL_MFMA 0
-#endif
-// A/B: issue priority NR_STREAM_PRIO outside the stream, 0 inside it (0 = no priority change)
-#ifndef NR_STREAM_PRIO
-#define NR_STREAM_PRIO 0
-#endif
 
 // Input layer + 7 hidden layers + the final layer's operand conversion of four 32-point tiles as
 // one software-pipelined instruction stream: tile t + 1's conversions issue beside tile t's MFMAs
@@ -664,18 +569,9 @@ __device__ __forceinline__ void mlp7_x4_stream(const uint16_t *__restrict__ lp, 
       "=&{v[104:111]}"(ab1), "=&{v[112:127]}"(bb0), "=&{v[128:143]}"(bb1)                                          \
     : [va] "v"(va), [vb] "v"(vb)                                                                                   \
     : "memory"
-#if NR_STREAM_PRIO
-#define NR_SP_IN "s_setprio 0\n"
-#else
-#define NR_SP_IN ""
-#endif
-    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_SP_IN NR_HID7_BF16_CLAMP NR_STREAM_OPERANDS);
-    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_SP_IN NR_HID7_BF16_MAX NR_STREAM_OPERANDS);
-    else asm volatile(NR_SP_IN NR_HID7_F16_MAX NR_STREAM_OPERANDS);
-#undef NR_SP_IN
-#if NR_STREAM_PRIO
-    __builtin_amdgcn_s_setprio(NR_STREAM_PRIO);
-#endif
+    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_HID7_BF16_CLAMP NR_STREAM_OPERANDS);
+    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_HID7_BF16_MAX NR_STREAM_OPERANDS);
+    else asm volatile(NR_HID7_F16_MAX NR_STREAM_OPERANDS);
 #undef NR_STREAM_OPERANDS
 }
 
@@ -687,7 +583,7 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
-    if constexpr (NR_LP_STREAM && NH == 7 && !NR_LP_FINAL_MFMA) {
+    if constexpr (NH == 7) {
         if (stream) {
             u32x4 kk[4][2];
 #pragma unroll
@@ -765,25 +661,6 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
     const float bf = fl[32 + 32 * nh];
     v8 k[4][2];
     relu_pack_tiles<PREC, 4, CL>(acc, k);
-#if NR_LP_FINAL_MFMA
-    // A/B: the final layer as 2 MFMAs per tile with the weights as row 0 of the A operand
-    // (lanes 0 and 32), the point's value in register 0 of lanes 0-31
-    const bool row0 = (lane & 31) == 0;
-    const v8 A0 = __builtin_bit_cast(v8, row0 ? wf[0] : (u32x4){0u, 0u, 0u, 0u});
-    const v8 A1 = __builtin_bit_cast(v8, row0 ? wf[1] : (u32x4){0u, 0u, 0u, 0u});
-    float zt[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const f32x16 zero = {};
-        zt[t] = mfma32<PREC>(A1, k[t][1], mfma32<PREC>(A0, k[t][0], zero))[0];
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zt[2 * s]), __float_as_uint(zt[2 * s + 1]), false,
-                                                        false);
-        out[s] = __uint_as_float(r[0]) + bf;
-    }
-#else
     float zt[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -802,7 +679,6 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
                                                         false);
         out[s] = (__uint_as_float(r[0]) + __uint_as_float(r[1])) + bf;
     }
-#endif
 }
 
 template <int PREC, bool CL>
@@ -815,12 +691,11 @@ __device__ __forceinline__ void mlp128_lowp_cl(const uint16_t *__restrict__ lp, 
 
 template <int PREC, bool CL>
 __device__ __forceinline__ float mlp16_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                               int nh, float fr, float x, float y, float z, uint32_t tmask,
-                                               bool stream) {
+                                               int nh, float fr, float x, float y, float z, uint32_t tmask) {
     // the bundled networks' depth (7 hidden layers) fully unrolled: no loop-carried
     // accumulator copies between layers
     if (nh == 7) {
-        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7, CL>(lp, fl, in0, nh, fr, x, y, z, stream);
+        if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
         return mlp32_lowp_nt<PREC, 1, 7, CL>(lp, fl, in0, nh, fr, x, y, z);
     }
     if (tmask & 0xcu) return mlp32_lowp_nt<PREC, 2, 0, CL>(lp, fl, in0, nh, fr, x, y, z);
@@ -829,16 +704,14 @@ __device__ __forceinline__ float mlp16_lowp_cl(const uint16_t *__restrict__ lp, 
 
 // tmask: the caller's 16-point tiles (bits 0-3); the 32-point tiles cover pairs of them.
 // cl (wave-uniform): the clamped-ReLU form is valid -- the pack is clamped (M.lp_clamp) and
-// every input of the call is within LP_INPUT_BOUND.  stream: M.lp_stream (two tiles of a
-// 7-hidden-layer network take the pipelined stream)
+// every input of the call is within LP_INPUT_BOUND
 template <int PREC>
 __device__ __forceinline__ float mlp16_lowp(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
-                                            int nh, float fr, float x, float y, float z, uint32_t tmask, bool cl,
-                                            bool stream) {
+                                            int nh, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
     if constexpr (PREC == NR_PRECISION_BF16) {
-        if (cl) return mlp16_lowp_cl<PREC, true>(lp, fl, in0, nh, fr, x, y, z, tmask, stream);
+        if (cl) return mlp16_lowp_cl<PREC, true>(lp, fl, in0, nh, fr, x, y, z, tmask);
     }
-    return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask, stream);
+    return mlp16_lowp_cl<PREC, false>(lp, fl, in0, nh, fr, x, y, z, tmask);
 }
 
 // ---- fp32x3: fp32-class hidden layers on the fp16 matrix core (NR_PRECISION_FP32X3).
@@ -988,8 +861,10 @@ __device__ __forceinline__ float mlp16_x3_split(const MlpArgs &M, const uint16_t
 __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, const uint16_t *lp, const float *fl,
                                           float fr, float x, float y, float z, uint32_t tmask, bool ok) {
     if (!ok) return mlp16_fp32(M, s32, fr, x, y, z, tmask);
+    // the frame is an input only of a 4-input network (a 3-input network's single-frame tracer
+    // passes A.frame here too: ADVICE r4)
     const bool in = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
-                    __builtin_fabsf(z) <= X3_INPUT_BOUND && __builtin_fabsf(fr) <= X3_FRAME_BOUND;
+                    __builtin_fabsf(z) <= X3_INPUT_BOUND && (M.in0 != 4 || __builtin_fabsf(fr) <= X3_FRAME_BOUND);
     const uint64_t out = __ballot(!in), live = __ballot(in);
     if (out == 0) return mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
     const float v32 = mlp16_fp32(M, s32, fr, x, y, z, tmask);
@@ -998,11 +873,6 @@ __device__ __forceinline__ float mlp16_x3(const MlpArgs &M, const float *s32, co
     return in ? v3 : v32;
 }
 
-// the tracers' x3 normals on 64 points: 1 = two one-tile passes (28 -> 9 spilled VGPRs in the bf16
-// batch tracer; C3 -1.7 %, profiles/r4_ab_x3_tiles.txt), 2 = one two-tile pass
-#ifndef NR_X3_NORMAL_TILES
-#define NR_X3_NORMAL_TILES 1
-#endif
 // The fp32 MLP as a call: the bf16/fp16 tracers' normals for points outside the x3 pack's input
 // bounds (never the bundled scenes' hit points).  Out of line, so that the fallback adds nothing
 // to the tracer's register demand at the shading site (inlined beside the split: 86 spilled VGPRs
@@ -1024,9 +894,10 @@ __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *
         v = mlp16_fp32_call(s32, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
     if (__ballot(in) != 0) {
         float v3;
-        if (NR_X3_NORMAL_TILES == 1 && (tmask & 0xcu)) {
+        if (tmask & 0xcu) {
             // two one-tile passes instead of one two-tile pass (fewer live registers at the
-            // shading site): the second on tile 1's points moved to lanes 0-31
+            // shading site: 28 -> 9 spilled VGPRs in the bf16 batch tracer, C3 -1.7 %,
+            // profiles/r4_ab_x3_tiles.txt): the second on tile 1's points moved to lanes 0-31
             v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, 0x3u);
             float a0, a1, b0, b1, c0, c1, d0, d1;
             half_views(x, a0, a1);
@@ -1037,28 +908,19 @@ __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *
             const float v1 = mlp16_x3_split(M, lp, fl, lo ? d1 : d0, lo ? a1 : a0, lo ? b1 : b0, lo ? c1 : c0, 0x3u);
             v3 = lo ? v3 : v1;
         } else {
-            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
+            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, 0x3u);
         }
         v = in ? v3 : v;
     }
     return v;
 }
 
-// The two-tile stream in the tracer's march (A/B knob, off): one wave alone runs the 64-point MLP
-// in 1,964 instead of 2,308 cycles, but the stream's 96 pinned registers push the tracer's live
-// state into scratch (bf16 batch: 8 -> 38 spilled VGPRs) and C3 runs 1.52 instead of 1.39 ms per
-// frame (profiles/r4_ab_stream.txt)
-#ifndef NR_TRACE_STREAM
-#define NR_TRACE_STREAM 0
-#endif
-
 // cl: see mlp16_lowp (ignored in fp32); fp32x3: the pack is valid (M.lp_clamp), the inputs are
 // checked here
 __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const uint16_t *slp, const float *sfl,
                                        int prec, float fr, float x, float y, float z, uint32_t tmask, bool cl) {
-    const bool stream = NR_TRACE_STREAM && M.lp_stream != 0;
-    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl, stream);
-    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl, stream);
+    if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
+    if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP32X3) return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0);
     return mlp16_fp32(M, s32, fr, x, y, z, tmask);
 }

@@ -39,90 +39,54 @@ namespace nr {
 #ifndef NR_TRACE_BPC_LOWP
 #define NR_TRACE_BPC_LOWP NR_TRACE_BPC_WIDE
 #endif
-#ifndef NR_RING_LOWP
-#define NR_RING_LOWP 64
-#endif
-#ifndef NR_SHADE_RAYS_LOWP
-#define NR_SHADE_RAYS_LOWP 16
-#endif
+constexpr int NR_RING_LOWP = 64;
+constexpr int NR_SHADE_RAYS_LOWP = 16;
 // the bulk-generating tracers keep each marching ray's direction and pixel in LDS (one float4
 // per lane, read back by the step) instead of four VGPRs live across the MLP
-#ifndef NR_RAY_D_LDS
-#define NR_RAY_D_LDS 1
-#endif
+constexpr int NR_RAY_D_LDS = 1;
 
 // Issue priority of a wave outside its MLP (scene, step, refill, shading).  A wave there
 // issues VALU in the shadows of the other waves' MFMAs instead of waiting behind them
 // (issue arbitration is priority, then age), so it is back in its MLP sooner and the
 // matrix pipe idles less: fp32 batch 2.050 -> 2.012 ms/frame (prio 1/2/3: 2.018/2.016/
 // 2.012; profiles/r1_ab_experiments.txt).  0 = off.  fp32 only (bf16: +1%).
-#ifndef NR_NONMLP_PRIO
-#define NR_NONMLP_PRIO 3
-#endif
+constexpr int NR_NONMLP_PRIO = 3;
 
 // bf16/fp16: issue priority NR_MLP_PRIO_LOWP inside the march MLP (the age-ordered arbitration
-// otherwise lets an older wave's scene/refill VALU cut into a younger wave's MFMA chain), and
-// NR_SHADE_PRIO_LOWP inside the shading pass's fp32 MLP, 0 elsewhere (0 = no change).  Alternating
-// A/B (tools/ab_trace_rounds.sh, profiles/r4_ab_prio.txt): march 2 -> C3 batch 1.370 / 1.389 vs
-// 1.379 / 1.405 ms, C5 1.410 / 1.417 vs 1.437 / 1.421; the shading priority, either alone or with
-// it, and 3 workgroups per CU were no better
-#ifndef NR_MLP_PRIO_LOWP
-#define NR_MLP_PRIO_LOWP 2
-#endif
-#ifndef NR_SHADE_PRIO_LOWP
-#define NR_SHADE_PRIO_LOWP 0
-#endif
+// otherwise lets an older wave's scene/refill VALU cut into a younger wave's MFMA chain), 0
+// elsewhere.  Alternating A/B (tools/ab_trace_rounds.sh, profiles/r4_ab_prio.txt): march 2 -> C3
+// batch 1.370 / 1.389 vs 1.379 / 1.405 ms, C5 1.410 / 1.417 vs 1.437 / 1.421; a priority in the
+// shading pass, either alone or with it, and 3 workgroups per CU were no better
+constexpr int NR_MLP_PRIO_LOWP = 2;
 
 
 // Wave-private pools of pixel-queue positions reserved one atomic ahead (bf16/fp16
 // tracers only: their iterations are short, so the ~1 us reservation latency is a large
 // part of the refill; the fp32 tracer's MLP hides it and the pools only lengthen the
 // tail -- tools/ab_multi.sh, profiles/r1_ab_experiments.txt).
-#ifndef NR_QUEUE_PREFETCH_LOWP
-#define NR_QUEUE_PREFETCH_LOWP 1
-#endif
-#ifndef NR_QUEUE_PREFETCH_FP32
-#define NR_QUEUE_PREFETCH_FP32 0
-#endif
-#ifndef NR_QUEUE_CHUNK
-#define NR_QUEUE_CHUNK 32
-#endif
-#ifndef NR_QUEUE_LOW
-#define NR_QUEUE_LOW 8
-#endif
+constexpr int NR_QUEUE_PREFETCH_LOWP = 1;
+constexpr int NR_QUEUE_PREFETCH_FP32 = 0;
+constexpr int NR_QUEUE_CHUNK = 32;
+constexpr int NR_QUEUE_LOW = 8;
 
-#ifndef NR_DENSE_GEN
-#define NR_DENSE_GEN 1
-#endif
+constexpr int NR_DENSE_GEN = 1;
 // Bulk generation's queue reservations (round 3): up to two ranges per generation (what is
 // left of the wave's pool + the pending reservation), chunks of NR_QUEUE_CHUNK_DENSE positions
 // requested whenever the pool holds fewer than that -- launches of >= 4 frames; launches of
 // fewer take chunks of NR_QUEUE_CHUNK_DENSE1, since positions a wave holds ahead lengthen a
 // single frame's tail (tools/ab_lowp.sh, profiles/r3_ab_experiments.txt (17)).
-#ifndef NR_QUEUE_TWO_RANGES
-#define NR_QUEUE_TWO_RANGES 1
-#endif
-#ifndef NR_QUEUE_CHUNK_DENSE
-#define NR_QUEUE_CHUNK_DENSE 64
-#endif
-#ifndef NR_QUEUE_CHUNK_DENSE1
-#define NR_QUEUE_CHUNK_DENSE1 32
-#endif
+constexpr int NR_QUEUE_TWO_RANGES = 1;
+constexpr int NR_QUEUE_CHUNK_DENSE = 64;
+constexpr int NR_QUEUE_CHUNK_DENSE1 = 32;
 // (fp32: A/B only -- its ring would cost the batched instance its fourth workgroup per CU)
-#ifndef NR_DENSE_GEN_FP32
-#define NR_DENSE_GEN_FP32 0
-#endif
+constexpr int NR_DENSE_GEN_FP32 = 0;
 
 // Refill only once this many ray slots are free (or the wave is empty), so that the ray
 // generation and the queue bookkeeping are paid for several rays at a time: bf16 batch
 // 0.611 -> 0.571 ms/frame at 8 (4: 0.589, 16: 0.575), fp32 1.978 -> 1.964 at 4
 // (profiles/r1_ab_experiments.txt).
-#ifndef NR_REFILL_MIN_LOWP
-#define NR_REFILL_MIN_LOWP 8
-#endif
-#ifndef NR_REFILL_MIN_FP32
-#define NR_REFILL_MIN_FP32 4
-#endif
+constexpr int NR_REFILL_MIN_LOWP = 8;
+constexpr int NR_REFILL_MIN_FP32 = 4;
 
 typedef __attribute__((address_space(1))) uint32_t *gptr_u32;
 
@@ -225,7 +189,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     constexpr bool QPF = PREC == NR_PRECISION_FP32 ? NR_QUEUE_PREFETCH_FP32 : NR_QUEUE_PREFETCH_LOWP;  // queue pools
     constexpr int NONMLP_PRIO = PREC == NR_PRECISION_FP32 ? NR_NONMLP_PRIO : 0;
     constexpr int MLP_PRIO = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16 ? NR_MLP_PRIO_LOWP : 0;
-    constexpr int SHADE_PRIO = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16 ? NR_SHADE_PRIO_LOWP : 0;
     constexpr int RMIN = PREC == NR_PRECISION_FP32 ? NR_REFILL_MIN_FP32 : NR_REFILL_MIN_LOWP;  // free slots per refill
     // rays generated in bulk through an LDS buffer (NR_DENSE_GEN): the reduced-precision tracers
     constexpr bool DENSE = NR_DENSE_GEN && (PREC != NR_PRECISION_FP32 || NR_DENSE_GEN_FP32) && !PROBE;
@@ -582,7 +545,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const F3 tp = mk3((qo == 0 || qo == 3) ? 1.0f : -1.0f, qo >= 2 ? 1.0f : -1.0f, (qo & 1) ? 1.0f : -1.0f);
             const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
             const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
-            if (SHADE_PRIO && !hold) set_priority(SHADE_PRIO);
             // NX3 (bf16/fp16, M.x3n): the normals in fp32x3 from the global-memory pack, whose
             // address is made opaque here so that its loop-invariant loads are not hoisted out of
             // the shading loop into registers held for the kernel's life
@@ -591,7 +553,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, M.x3lp + zoff_x3, M.x3fl + zoff_x3, fr_of(sfr), pq.x, pq.y,
                                                     pq.z, smask)
                                   : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
-            if (SHADE_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
             const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
             if (k < nb && q4 == 0 && !T.itmap) {
@@ -731,365 +692,6 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     }
 }
 
-// ---- The bf16/fp16 batched tracer with two ray groups per wave (round 4) ----
-// Every lane holds two ray slots (group s = 0, 1: slot s * 64 + lane), so a wave marches up to 128
-// rays and, while both groups have live rays, evaluates them as one 128-point MLP (mlp32_lowp_128:
-// four 32-point tiles, the pipelined stream, the k_mlp16 form) instead of two 64-point ones.  The
-// per-ray arithmetic is k_trace's, bit for bit (the 128-point form equals the 64-point form per
-// point; tests/test_gpu_stream.py); only the grouping changes.  The rest of the iteration -- refill
-// from the LDS ray ring, the shading passes, the scene and the step -- runs on both groups.  Three
-// workgroups per CU: the stream pins 144 of the 168 VGPRs, so only the rays' positions and
-// iteration counts stay in registers across it; direction, pixel, tfar and frame live in LDS.
-// Used for batched bf16/fp16 launches of 64 rays per wave (launch_trace; nr_set_debug bit 14:
-// k_trace).
-constexpr int STASH2 = 16 - 1 + 128;  // a shading pass leaves at most 15 rays; one iteration adds <= 128
-template <int PREC, bool NX3 = false>
-__global__ __launch_bounds__(256, 3) void k_trace2(RenderArgs A, MlpArgs M, TraceArgs T) {
-    static_assert(PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16, "reduced precision only");
-    constexpr int RMIN = NR_REFILL_MIN_LOWP;
-    constexpr int RB = NR_RING_LOWP;
-    const uint32_t QCHUNK = T.nframes >= 4 ? NR_QUEUE_CHUNK_DENSE : NR_QUEUE_CHUNK_DENSE1;
-    const uint32_t QLOW = QCHUNK;
-    __shared__ FrameLds sf[NR_MAX_BATCH];
-    for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // as k_trace's
-        const int f = i / 18, w = i - 18 * f;
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(T.frames + f);
-        reinterpret_cast<uint32_t *>(sf + f)[w] = w < 12 ? src[w] : (w < 16 ? src[16 + w] : (w == 16 ? src[32] : 0u));
-    }
-    Smem16 S = stage16<PREC, true>(M);
-    __shared__ float4 stash[4][STASH2];
-    __shared__ uint8_t stash_f[4][STASH2];
-    __shared__ float4 rbuf_p[4][RB], rbuf_d[4][RB];
-    __shared__ uint8_t rbuf_f[4][RB];
-    __shared__ float4 ray_dp[4][128];  // slot s * 64 + lane: {d.xyz, pixel}
-    __shared__ float2 ray_tr[4][128];  // {tfar, frame}
-    const int lane = lane_id();
-    const int wid = threadIdx.x >> 6;
-    const long nchunks = T.nblocks;
-    const auto rq = __builtin_amdgcn_make_buffer_rsrc(T.pix_ctr, 0, 128 << T.nq_shift, 0x00020000);
-    auto out_of = [&](int f) -> gptr_u32 { return (gptr_u32)sf[f].out; };
-    auto fr_of = [&](int f) -> float { return M.in0 == 4 ? sf[f].frame_f : 0.0f; };
-    auto put = [&](int f, uint32_t i, uint32_t v) { out_of(f)[i] = v; };
-    int nstash = 0;
-    const int nq = 1 << T.nq_shift;
-    int shard = blockIdx.x & (nq - 1), tries = 0;
-    bool qempty = false;
-    uint32_t pool_base = 0, pool_cnt = 0, pend_v = 0;
-    bool pend = false;
-    uint32_t rb_n = 0, rb_head = 0;
-    F3 p[2] = {mk3(0, 0, 0), mk3(0, 0, 0)};
-    int it[2] = {-1, -1};
-    int maxit = 0;
-    uint32_t nsteps = 0, nhit = 0, nconv = 0;
-    auto shard_total = [&](int sh) -> long {
-        const long sh_chunks = sh < nchunks ? ((nchunks - 1 - sh) >> T.nq_shift) + 1 : 0;
-        return sh_chunks * 64 * T.nframes;
-    };
-    // the frame f and pixel (px, py) of queue position q (k_trace's pixel_of, batched, not a probe)
-    auto pixel_of = [&](uint32_t q, int &f, int &px, int &py) -> bool {
-        if (T.interleave) {
-            const uint32_t c = q >> 6, cq = udiv_r(c, (uint32_t)T.nframes, T.inv_nframes);
-            f = (int)(c - cq * (uint32_t)T.nframes);
-            q = (cq << 6) | (q & 63u);
-        } else {
-            const uint32_t per = (uint32_t)((((nchunks - 1 - shard) >> T.nq_shift) + 1) * 64);
-            f = (int)udiv_r(q, per, 1.0 / (double)per);
-            q -= (uint32_t)f * per;
-        }
-        uint32_t bq = q >> 6, pq = q & 63;
-        if (T.spread_shift) {
-            const int sh = T.spread_shift;
-            const uint32_t G = 1u << sh;
-            const uint32_t sh_chunks = (uint32_t)(((nchunks - 1 - shard) >> T.nq_shift) + 1);
-            const uint32_t g = q >> (6 + sh), r = q & ((64u << sh) - 1u);
-            const uint32_t nbg = min(G, sh_chunks - g * G);
-            pq = nbg == G ? r >> sh : r / nbg;
-            bq = g * G + (r - pq * nbg);
-        }
-        const long pos = ((long)bq << T.nq_shift) + shard;
-        const int blk = T.order ? (int)T.order[pos] : (int)pos;
-        const int by = (int)udiv_r((uint32_t)blk, (uint32_t)T.bw, T.inv_bw), bx = blk - by * T.bw;
-        px = bx * 8 + (pq & 7);
-        py = by * 8 + (pq >> 3);
-        return px < A.W && py < A.rows;
-    };
-    while (true) {
-        // the lane index as an opaque per-iteration value: the LDS addresses formed from it are then
-        // formed where they are used, not hoisted out of the loop into registers held across the
-        // MLP stream (which pins 144 of the 168 VGPRs)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        nstash = __builtin_amdgcn_readfirstlane(nstash);
-        qempty = __builtin_amdgcn_readfirstlane((int)qempty) != 0;
-        shard = __builtin_amdgcn_readfirstlane(shard);
-        tries = __builtin_amdgcn_readfirstlane(tries);
-        pool_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_base);
-        pool_cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)pool_cnt);
-        pend = __builtin_amdgcn_readfirstlane((int)pend) != 0;
-        rb_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_n);
-        rb_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_head);
-        // ---- refill the free slots of both groups from the ring (generated in bulk)
-        if (!qempty || rb_n > 0) {
-            const uint64_t free0 = __ballot(it[0] < 0), free1 = __ballot(it[1] < 0);
-            const uint32_t n0 = (uint32_t)__popcll(free0), nfree = n0 + (uint32_t)__popcll(free1);
-            if (nfree >= (uint32_t)RMIN || (qempty && nfree)) {
-                if (rb_n < nfree && rb_n < (uint32_t)RB && !qempty) {
-                    // up to two ranges of queue positions: the pool's rest, then the pending
-                    // reservation; a blocking reservation only when both are empty (k_trace's)
-                    uint32_t base = 0, got = 0, base2 = 0, got2 = 0;
-                    const uint32_t want = (uint32_t)RB - rb_n;
-                    if (pool_cnt) {
-                        base = pool_base;
-                        got = min(want, pool_cnt);
-                        pool_base += got;
-                        pool_cnt -= got;
-                    }
-                    if (got < want) {
-                        if (pend) {
-                            const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)pend_v);
-                            pend = false;
-                            const long tot = shard_total(shard);
-                            if ((long)b < tot) {
-                                pool_base = b;
-                                pool_cnt = (uint32_t)min((long)QCHUNK, tot - (long)b);
-                            }
-                        }
-                        if (pool_cnt == 0 && got == 0) {
-                            while (true) {  // nothing reserved: a blocking reservation
-                                const long tot = shard_total(shard);
-                                const uint32_t w = max(want, QCHUNK);
-                                const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)queue_add(rq, lane, shard, w));
-                                if ((long)b < tot) {
-                                    pool_base = b;
-                                    pool_cnt = (uint32_t)min((long)w, tot - (long)b);
-                                    break;
-                                }
-                                shard = (shard + 1) & (nq - 1);
-                                if (++tries >= nq) {
-                                    qempty = true;
-                                    break;
-                                }
-                            }
-                            if (pool_cnt) {
-                                base = pool_base;
-                                got = min(want, pool_cnt);
-                                pool_base += got;
-                                pool_cnt -= got;
-                            }
-                        } else if (pool_cnt) {
-                            base2 = pool_base;
-                            got2 = min(want - got, pool_cnt);
-                            pool_base += got2;
-                            pool_cnt -= got2;
-                        }
-                    }
-                    if (!qempty && !pend && pool_cnt < QLOW) {
-                        pend_v = queue_add(rq, lane, shard, QCHUNK);
-                        pend = true;
-                    }
-                    bool hit = false, keep = false;
-                    F3 gp = mk3(0.0f, 0.0f, 0.0f), gd = mk3(0.0f, 0.0f, 0.0f);
-                    float gt = 0.0f;
-                    uint32_t glp = 0;
-                    int gf = 0;
-                    if ((uint32_t)lane < got + got2) {
-                        int px, py;
-                        const uint32_t qpos = (uint32_t)lane < got ? base + (uint32_t)lane : base2 + ((uint32_t)lane - got);
-                        if (pixel_of(qpos, gf, px, py)) {
-                            glp = (uint32_t)((long)py * A.W + px);
-                            hit = gen_ray(A, T, sf[gf].inv_view, px, py, gp, gd, gt);
-                            keep = hit && A.max_steps > 0;
-                            if (!keep) put(gf, glp, 0u);
-                        }
-                    }
-                    nhit += (uint32_t)__popcll(__ballot(hit));
-                    const uint64_t km = __ballot(keep);
-                    if (keep) {
-                        const uint32_t slot = (rb_head + rb_n + rank_below(km)) & (uint32_t)(RB - 1);
-                        rbuf_p[wid][slot] = make_float4(gp.x, gp.y, gp.z, gt);
-                        rbuf_d[wid][slot] = make_float4(gd.x, gd.y, gd.z, __uint_as_float(glp));
-                        rbuf_f[wid][slot] = (uint8_t)gf;
-                    }
-                    rb_n += (uint32_t)__popcll(km);
-                }
-                // deal: group 0's free slots first, then group 1's, in ring order
-                const uint32_t take = min(nfree, rb_n);
-                if (take) {
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        const uint32_t rank = (s ? n0 : 0u) + rank_below(s ? free1 : free0);
-                        if (it[s] < 0 && rank < take) {
-                            const uint32_t slot = (rb_head + rank) & (uint32_t)(RB - 1);
-                            const float4 ra = rbuf_p[wid][slot];
-                            p[s] = mk3(ra.x, ra.y, ra.z);
-                            ray_dp[wid][64 * s + ln] = rbuf_d[wid][slot];
-                            ray_tr[wid][64 * s + ln] = make_float2(ra.w, __int_as_float((int)rbuf_f[wid][slot]));
-                            it[s] = 0;
-                        }
-                    }
-                    rb_head = (rb_head + take) & (uint32_t)(RB - 1);
-                    rb_n -= take;
-                }
-            }
-        }
-        const bool drained = qempty && rb_n == 0;
-        // ---- colour stashed converged rays, 16 per pass (k_trace's)
-        uint64_t lm0 = __ballot(it[0] >= 0), lm1 = __ballot(it[1] >= 0);
-        constexpr int SHR = NR_SHADE_RAYS_LOWP;
-        while (nstash >= SHR || (drained && nstash > 0 && !(lm0 | lm1))) {
-            const int nb = min(SHR, nstash);
-            const int k = lane >> 2;
-            const int e = nstash - nb + (k < nb ? k : 0);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            const float4 sp = stash[wid][e];
-            const int sfr = (int)stash_f[wid][e];
-            const int qo = ln & 3;
-            const F3 tp = mk3((qo == 0 || qo == 3) ? 1.0f : -1.0f, qo >= 2 ? 1.0f : -1.0f, (qo & 1) ? 1.0f : -1.0f);
-            const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
-            const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
-            if (NR_SHADE_PRIO_LOWP) set_priority(NR_SHADE_PRIO_LOWP);
-            int zoff_x3 = 0;  // (as k_trace's)
-            if constexpr (NX3) asm volatile("" : "+s"(zoff_x3));
-            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, M.x3lp + zoff_x3, M.x3fl + zoff_x3, fr_of(sfr), pq.x, pq.y,
-                                                    pq.z, smask)
-                                  : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
-            if (NR_SHADE_PRIO_LOWP) __builtin_amdgcn_s_setprio(0);
-            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, sf[sfr].zoff));
-            const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
-            if (k < nb && qo == 0 && !T.itmap) {
-                const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                const uint32_t pxl = __float_as_uint(sp.w);
-                F3 rd = mk3(0.0f, 0.0f, 0.0f);
-                if (A.color_type == NR_COLOR_FACING) {
-                    const int lr = (int)udiv_r(pxl, (uint32_t)A.W, A.inv_w);
-                    rd = ray_dir(A, T, sf[sfr].inv_view, (int)(pxl - (uint32_t)lr * A.W), lr);
-                }
-                const float *nmx = (const float *)((const __attribute__((address_space(1))) float *)T.frames[sfr].normal);
-                put(sfr, pxl, shade_color(A, nmx, nrm, rd));
-            }
-            nconv += (uint32_t)nb;
-            nstash -= nb;
-        }
-        if (!(lm0 | lm1)) {
-            if (drained && nstash == 0) break;
-            continue;
-        }
-        // ---- the tail: once the queue has drained and both groups fit one, move group 1's rays
-        // into group 0 (lane i takes the i-th live ray, group 0's first), then pack group 0 into
-        // its lowest tiles -- so the tail marches ceil(live / 16) tiles, as k_trace's does
-        if (drained) {
-            const int n0 = (int)__popcll(lm0), n1 = (int)__popcll(lm1), nl = n0 + n1;
-            if (nl <= 64 && (n1 > 0 || __popc(tiles_of(lm0)) > ((n0 + 15) >> 4))) {
-                const bool from1 = lane >= n0 && lane < nl;
-                const int src = lane < nl ? select_bit(from1 ? lm1 : lm0, from1 ? lane - n0 : lane) : lane;
-                const F3 a0 = mk3(__shfl(p[0].x, src), __shfl(p[0].y, src), __shfl(p[0].z, src));
-                const F3 a1 = mk3(__shfl(p[1].x, src), __shfl(p[1].y, src), __shfl(p[1].z, src));
-                const int i0 = __shfl(it[0], src), i1 = __shfl(it[1], src);
-                const float4 dp = ray_dp[wid][64 * (from1 ? 1 : 0) + src];
-                const float2 tr = ray_tr[wid][64 * (from1 ? 1 : 0) + src];
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                p[0] = from1 ? a1 : a0;
-                it[0] = lane < nl ? (from1 ? i1 : i0) : -1;
-                it[1] = -1;
-                ray_dp[wid][ln] = dp;
-                ray_tr[wid][ln] = tr;
-                lm0 = __ballot(it[0] >= 0);
-                lm1 = 0;
-            }
-        }
-        // ---- the MLP on every live point: one 128-point evaluation while both groups march
-        float sdf[2];
-        if (NR_MLP_PRIO_LOWP) set_priority(NR_MLP_PRIO_LOWP);
-        // the rays' frames' animation input (4-input networks only)
-        auto frame_in = [&](int s) -> float {
-            return M.in0 == 4 ? fr_of(__float_as_int(ray_tr[wid][64 * s + ln].y)) : 0.0f;
-        };
-        if (lm0 && lm1) {
-            const float fr[2] = {frame_in(0), frame_in(1)};
-            const float x[2] = {p[0].x, p[1].x}, y[2] = {p[0].y, p[1].y}, z[2] = {p[0].z, p[1].z};
-            if (PREC == NR_PRECISION_BF16 && M.lp_clamp)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, M.in0, M.nh, fr, x, y, z, sdf, M.lp_stream != 0);
-            else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, M.in0, M.nh, fr, x, y, z, sdf, M.lp_stream != 0);
-        } else {
-            const int s = lm0 ? 0 : 1;
-            const F3 ps = s ? p[1] : p[0];
-            sdf[0] = sdf[1] = mlp16(M, S.s32, S.slp, S.sfl, PREC, frame_in(s), ps.x, ps.y, ps.z, tiles_of(s ? lm1 : lm0),
-                                    M.lp_clamp != 0);
-        }
-        if (NR_MLP_PRIO_LOWP) __builtin_amdgcn_s_setprio(0);
-        nsteps += (uint32_t)(__popcll(lm0) + __popcll(lm1));
-        if (nsteps >= (1u << 30)) {
-            if (lane == 0) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
-            nsteps = 0;
-        }
-        // ---- one sphere-trace step per ray of both groups (k_trace's)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bool conv = false;
-            uint32_t pix = 0;
-            int rfs = 0;
-            if (it[s] >= 0) {
-                const float2 tr = ray_tr[wid][64 * s + ln];
-                rfs = __float_as_int(tr.y);
-                const float ts = scene_sdf(p[s], sdf[s], A.scene, sf[rfs].zoff);
-                const float4 dp = ray_dp[wid][64 * s + ln];
-                const F3 d = mk3(dp.x, dp.y, dp.z);
-                pix = __float_as_uint(dp.w);
-                const float tf = tr.x - ts;
-                ray_tr[wid][64 * s + ln].x = tf;
-                int used = 0;
-                if (tf <= 0) {
-                    put(rfs, pix, 0u);
-                    used = it[s] + 1;
-                } else {
-                    p[s] = add3(p[s], mul3s(d, ts));
-                    if (ts < MARCHING_EPSILON) {
-                        if (it[s] + 1 < A.max_steps) {
-                            conv = true;
-                            used = it[s] + 2;
-                        } else {
-                            put(rfs, pix, 0u);
-                            used = it[s] + 1;
-                        }
-                    } else if (++it[s] >= A.max_steps) {
-                        put(rfs, pix, 0u);
-                        used = A.max_steps;
-                    }
-                }
-                if (used) {
-                    it[s] = -1;
-                    maxit = max(maxit, used);
-                    if (T.itmap) put(rfs, pix, (uint32_t)used);
-                    if (T.bcost) {
-                        const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
-                        atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
-                    }
-                }
-            }
-            const uint64_t cm = __ballot(conv);
-            if (conv) {
-                const int slot = nstash + (int)rank_below(cm);
-                stash[wid][slot] = make_float4(p[s].x, p[s].y, p[s].z, __uint_as_float(pix));
-                stash_f[wid][slot] = (uint8_t)rfs;
-            }
-            nstash += (int)__popcll(cm);
-        }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
-    if (lane == 0) {
-        if (nsteps) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
-        if (nhit) atomicAdd(T.stats + 1, (unsigned long long)nhit);
-        if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
-        if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
-    }
-}
-
-#ifndef NR_MLP16_PRIO
-#define NR_MLP16_PRIO 0
-#endif
 // diagnostic build (tools/mlp_stamps.py): per-wave cycle stamps of the 16-bit k_mlp16 loop in Y
 #ifndef NR_MLP16_STAMPS
 #define NR_MLP16_STAMPS 0
@@ -1119,23 +721,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_of(const void *p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
 // IN0: the network's inputs (3, or 4 with the frame): a template parameter, so that the load is
-// not behind a branch (whose join waited for it).  CUQ (bf16/fp16): one workgroup of 12 waves per
-// CU (3 per SIMD, every wave of the CU in it) dealing its share of the chunks through an LDS counter
-// (see the chunk loop); otherwise 4-wave workgroups dealing chunks grid-stride.
-template <int PREC, int IN0, bool CUQ = false>
-__global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
-                                    : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, int n) {
-    constexpr int WPG = CUQ ? 4 * NR_MLP16_WPS_LP : 4;  // waves per workgroup
-    __shared__ uint32_t cq[1];                           // CUQ: the workgroup's chunk counter
-    if (CUQ && threadIdx.x == 0) cq[0] = 0u;              // (stage16's barrier publishes it)
+// not behind a branch (whose join waited for it).  4-wave workgroups deal the chunks grid-stride.
+template <int PREC, int IN0>
+__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
+                                  : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, int n) {
+    constexpr int WPG = 4;  // waves per workgroup
     Smem16 S = stage16<PREC, false>(M);
     const int lane = lane_id();
     constexpr int in0 = IN0;
-    if constexpr (NR_MLP16_PRIO == 1 && PREC != NR_PRECISION_FP32) {
-        // A/B: static issue priority by the wave's slot on its SIMD (HW_ID.WAVE_ID), so that the
-        // co-resident waves do not march through their streams in step
-        set_priority((int)(__builtin_amdgcn_s_getreg((3 << 11) | 4) & 3u));
-    }
     M.in0 = IN0;
     const auto rx = buffer_of(X, (uint32_t)n * (uint32_t)in0 * 4u), ry = buffer_of(Y, (uint32_t)n * 4u);
     // point i's inputs (zeros past the end); the 4th is the frame for 4-input networks
@@ -1187,45 +780,16 @@ __global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PR
         unsigned long long st_mlp = 0;
         uint32_t st_n = 0;
 #endif
-        // Chunk dealing.  Grid-stride (4-wave workgroups, 3 per CU): a wave's chunks are wave, wave +
-        // waves, ...; but the oldest wave of each SIMD wins issue arbitration and runs its chunks at
-        // ~4,800 cycles against its neighbours' ~7,300, so it finishes its equal share at 2/3 of the
-        // loop and leaves the last third to two waves per SIMD (profiles/r4_mlp_stamps_hwid.txt).
-        // CUQ: the CU's 12 waves form one workgroup that owns a contiguous range of chunks and deals
-        // them one at a time through an LDS counter, so a faster wave simply takes more of them and
-        // the CU's waves finish within one chunk of each other.  (Dealing through global counters
-        // cost more than it balanced: one counter serialises its atomics at ~10 ns each, and even
-        // spread over 32 counters the claims' round trips stretched every chunk;
-        // profiles/r4_ab_dyn.txt.)  A claim is requested at the top of a chunk and read at its end.
+        // Chunk dealing, grid-stride: a wave's chunks are wave, wave + waves, ...  (The oldest wave
+        // of each SIMD wins issue arbitration and finishes its share at ~2/3 of the loop; balancing
+        // the CU's waves through an LDS chunk queue or global claims did not raise the chunk rate,
+        // round 4: profiles/r4_mlp_ab.txt, r4_ab_dyn.txt, r4_mlp_stamps_hwid.txt.)
         const uint32_t nch = (uint32_t)(nfull >> 7);
-        const int per = CUQ ? (int)((nch + gridDim.x - 1u) / gridDim.x) : 0;
-        const int lo = CUQ ? min((int)blockIdx.x * per, (int)nch) : 0, hi = CUQ ? min(lo + per, (int)nch) : 0;
         int gs = wave;
-        uint32_t claim_v = 0;  // CUQ: the claim requested at this chunk's top (lane 0's value)
-        int claim_s = 0;       // ... moved to a scalar register before the MLP (no VGPR held across it)
-        // every lane adds 1 (a wave-uniform operand: hipcc's atomic optimizer makes it one ds_add of
-        // 64 by the first lane, where a lane-dependent operand became a 64-step scan loop), so a
-        // claim advances the counter by 64 and is its value >> 6
-        auto claim = [&]() {
-            if constexpr (CUQ) claim_v = atomicAdd(&cq[0], 1u);
-        };
-        auto settle = [&]() {
-            if constexpr (CUQ) claim_s = __builtin_amdgcn_readfirstlane((int)claim_v) >> 6;
-        };
-        auto fixed = [&]() -> int {
-            if constexpr (CUQ) {
-                const int c = lo + claim_s;
-                return c < hi ? c : -1;
-            } else {
-                const int c = gs;
-                gs += waves;
-                return c < (int)nch ? c : -1;
-            }
-        };
         auto first = [&]() -> int {
-            claim();
-            settle();
-            return fixed();
+            const int c = gs;
+            gs += waves;
+            return c < (int)nch ? c : -1;
         };
         int cur = first(), nxt = first();
         float nx[2], ny[2], nz[2], nf[2];
@@ -1247,7 +811,6 @@ __global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PR
             // everything in flight was issued a chunk ago: wait for it all here (free), so that
             // hipcc's scoreboard holds nothing older than this iteration's own requests
             __builtin_amdgcn_s_waitcnt(0x0f70);
-            claim();  // the chunk after next (CUQ): settled below, consumed at this chunk's end
             const int base = cur * 128;
             const float x[2] = {nx[0], nx[1]}, y[2] = {ny[0], ny[1]}, z[2] = {nz[0], nz[1]}, f[2] = {nf[0], nf[1]};
             const int nb = (nxt < 0 ? (int)nch : nxt) * 128;  // past the last chunk: zeros, unused
@@ -1262,7 +825,6 @@ __global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PR
             const bool ok = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
                             __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
                             __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
-            settle();
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
                 mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
             else
@@ -1273,7 +835,7 @@ __global__ __launch_bounds__(CUQ ? 64 * 4 * NR_MLP16_WPS_LP : 256, PREC == NR_PR
 #endif
             pbase = base;
             cur = nxt;
-            nxt = fixed();
+            nxt = first();
         };
 #if NR_MLP16_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
@@ -1371,19 +933,12 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         const int m = (int)std::min(SEG, n - p0);
         const float *x = X + p0 * M.in0;
         float *y = Y + p0;
-        // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane);
-        // bf16/fp16 with the CU queue (M.lp_cuq): one 12-wave workgroup per CU (grid = CUs)
-        const bool cuq = lowp && M.lp_cuq > 0;
-        const long per_wg = cuq ? 128l * 4 * NR_MLP16_WPS_LP : lowp ? 512 : 256;
-        const int g = (int)std::max<long>(1, std::min<long>(cuq ? M.lp_cuq : grid, ((long)m + per_wg - 1) / per_wg));
-        const int threads = cuq ? 64 * 4 * NR_MLP16_WPS_LP : 256;
-        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(threads), sm, st, M, x, y, m); };
+        // points per workgroup: 4 waves x 64 (fp32, fp32x3) or x 128 (bf16, fp16: two per lane)
+        const long per_wg = lowp ? 512 : 256;
+        const int g = (int)std::max<long>(1, std::min<long>(grid, ((long)m + per_wg - 1) / per_wg));
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
         const bool four = M.in0 == 4;
-        if (prec == NR_PRECISION_BF16 && cuq)
-            four ? go(k_mlp16<NR_PRECISION_BF16, 4, true>) : go(k_mlp16<NR_PRECISION_BF16, 3, true>);
-        else if (prec == NR_PRECISION_FP16 && cuq)
-            four ? go(k_mlp16<NR_PRECISION_FP16, 4, true>) : go(k_mlp16<NR_PRECISION_FP16, 3, true>);
-        else if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
+        if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
         else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
         else if (prec == NR_PRECISION_FP32X3) four ? go(k_mlp16<NR_PRECISION_FP32X3, 4>) : go(k_mlp16<NR_PRECISION_FP32X3, 3>);
         else four ? go(k_mlp16<NR_PRECISION_FP32, 4>) : go(k_mlp16<NR_PRECISION_FP32, 3>);
@@ -1398,7 +953,7 @@ template <int PREC, bool PROBE, bool STAMPS, bool BATCH>
 static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, int sm,
                                  hipStream_t st) {
     constexpr bool LOWP = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16;
-    if constexpr (LOWP && NR_X3_NORMALS && !PROBE) {
+    if constexpr (LOWP && !PROBE) {
         if (M.x3n) {
             hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true>), dim3(grid), dim3(256), sm, st, A, M, T);
             return hipGetLastError();
@@ -1420,26 +975,6 @@ static hipError_t launch_trace_p(const RenderArgs &A, const MlpArgs &M, const Tr
 
 hipError_t launch_trace(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int prec, int grid, hipStream_t st) {
     const int sm = smem16_bytes(M, prec, true);
-    // the batched bf16/fp16 tracer with two ray groups per wave: 64 rays per group, no diagnostics
-    // or age hold (those keep k_trace), on the resident grid of 3 workgroups per CU
-    if (T.nframes > 0 && T.two_groups && !T.probe && !T.stamps && T.take >= 64 && T.hold_age == INT_MAX &&
-        (prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16)) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return hipErrorInvalidDevice;
-        const int g = std::max(1, std::min(grid, 3 * cus));
-        const bool x3 = NR_X3_NORMALS && M.x3n;
-        if (prec == NR_PRECISION_BF16 && x3)
-            hipLaunchKernelGGL((k_trace2<NR_PRECISION_BF16, true>), dim3(g), dim3(256), sm, st, A, M, T);
-        else if (prec == NR_PRECISION_BF16)
-            hipLaunchKernelGGL((k_trace2<NR_PRECISION_BF16>), dim3(g), dim3(256), sm, st, A, M, T);
-        else if (x3)
-            hipLaunchKernelGGL((k_trace2<NR_PRECISION_FP16, true>), dim3(g), dim3(256), sm, st, A, M, T);
-        else
-            hipLaunchKernelGGL((k_trace2<NR_PRECISION_FP16>), dim3(g), dim3(256), sm, st, A, M, T);
-        return hipGetLastError();
-    }
     if (T.probe) return launch_trace_p<true, false, false>(A, M, T, prec, grid, sm, st);
     if (T.nframes > 0) return launch_trace_p<false, false, true>(A, M, T, prec, grid, sm, st);
     if (T.stamps) return launch_trace_p<false, true, false>(A, M, T, prec, grid, sm, st);

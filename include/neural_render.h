@@ -235,11 +235,7 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected).  Bit 11 = the
  * bf16/fp16 MLP of 7-hidden-layer networks in its builtin-compiled form instead of the
  * software-pipelined instruction streams (nr_mlp16_asm.h; the same values, for A/B and parity).
- * Bit 12 = the bf16/fp16 nr_mlp_forward deals its 128-point chunks through one 12-wave workgroup
- * per CU with an LDS chunk queue instead of grid-stride over 4-wave workgroups (the same values;
- * A/B, equal speed).  Bit 14 = batched bf16/fp16 launches on the tracer with two ray groups per wave
- * (k_trace2: 128 rays per wave, one 128-point MLP per iteration) instead of k_trace (the same
- * pixels; A/B -- it is slower).  Bit 15 = the bf16/fp16 tracers' normals (the four tetrahedron
+ * Bit 15 = the bf16/fp16 tracers' normals (the four tetrahedron
  * samples of every coloured ray) by the fp32 MLP instead of the fp32x3 split (A/B; the frames'
  * march is the same, their shading moves by the two forms' rounding). */
 int nr_set_debug(nr_ctx *ctx, int flags);

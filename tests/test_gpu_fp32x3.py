@@ -239,3 +239,22 @@ def test_x3_batch_frames_straddling_bound():
         imgs, _ = r.render_batch(80, 64, [(iv, nm, f) for f in frames], 64)
     assert all(np.array_equal(a, b) for a, b in zip(imgs, singles))
     assert any((s != 0).any() for s in singles)
+
+
+def test_x3_three_input_net_past_frame_bound(chrome):
+    """A 3-input network at frame 2000 (> X3_FRAME_BOUND): the frame is not an input of the
+    network, so every point stays on the split -- the single-frame render (whose tracer passes the
+    frame number to the MLP), the batched render and the oracle's restatement agree."""
+    dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
+    iv, nm = nr.camera(20.0, 30.0, 2.0)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("plane_1")).set_precision("fp32x3")
+        r.set_view(iv, nm, 2000).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        img, st = r.render(96, 96, 64)
+        imgs, _ = r.render_batch(96, 96, [(iv, nm, 2000), (iv, nm, 2000)], 64)
+    pack = nr.pack_x3(dims, K, B)
+    net = oracle.OracleNet(K, B, x3_pack=pack[:2])
+    ref, rst = net.render(96, 96, iv, nm, frame=2000, color_type=1, matcap=chrome, max_steps=64, precision=4)
+    assert (ref != 0).any()
+    assert np.array_equal(img, ref) and st["ray_steps"] == rst["ray_steps"], (img != ref).sum()
+    assert all(np.array_equal(b, ref) for b in imgs)

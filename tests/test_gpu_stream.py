@@ -79,127 +79,3 @@ def test_mlp_stream_ragged(rend, nets, prec):
             assert np.array_equal(a, b), n
     finally:
         rend.set_precision("fp32")
-
-
-# ---- the tracer's march MLP (two 32-point tiles per wave: mlp7_x2_stream) -- whole frames
-
-@pytest.fixture(scope="module")
-def chrome():
-    return nr.load_png(nr.matcap_path("Chrome"))
-
-
-@pytest.mark.parametrize("prec,debug", [("bf16", 0), ("bf16", NO_CLAMP), ("fp16", 0)])
-@pytest.mark.parametrize("geom", ["plane_1", "car_1"])
-def test_trace_stream_frames_identical(rend, chrome, geom, prec, debug):
-    """One frame and a 6-frame batch (the batched instance) with the stream and with the builtin
-    form: every pixel identical, and the same ray-step counts."""
-    rend.load_h5(nr.geometry_path(geom)).set_precision(prec)
-    rend.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
-    cams = [nr.camera(5.0 * i, 30.0 * i, 2.0) + (i,) for i in range(6)]
-    rend.set_view(*cams[1][:2], 0)
-    try:
-        (a, sa), (b, sb) = stream_and_builtin(rend, lambda: rend.render(384, 320, 128), debug)
-        assert np.array_equal(a, b), int((a != b).sum())
-        assert sa["ray_steps"] == sb["ray_steps"]
-        (fa, _), (fb, _) = stream_and_builtin(rend, lambda: rend.render_batch(256, 256, cams, 96), debug)
-        for i, (x, y) in enumerate(zip(fa, fb)):
-            assert np.array_equal(x, y), (i, int((x != y).sum()))
-    finally:
-        rend.set_precision("fp32")
-
-
-def test_trace_stream_animation_frames_identical(rend, chrome):
-    """A 4-input network: the frame number rides in the stream's input operands."""
-    rng = np.random.default_rng(24)
-    dims = [4] + [32] * 8 + [1]
-    K = [(rng.standard_normal((dims[i], dims[i + 1])) / np.sqrt(dims[i])).astype(np.float32) for i in range(9)]
-    B = [(rng.standard_normal(dims[i + 1]) * 0.05).astype(np.float32) for i in range(9)]
-    B[-1][:] = 0.3
-    rend.load_mlp(dims, K, B).set_precision("bf16")
-    rend.set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
-    cams = [nr.camera(0.0, 10.0 * i, 2.0) + (7 * i,) for i in range(4)]
-    try:
-        (fa, sa), (fb, sb) = stream_and_builtin(rend, lambda: rend.render_batch(192, 160, cams, 64))
-        for i, (x, y) in enumerate(zip(fa, fb)):
-            assert np.array_equal(x, y), (i, int((x != y).sum()))
-        assert sa["ray_steps"] == sb["ray_steps"]
-    finally:
-        rend.set_static(nr.NR_COLOR_MATCAP, 3).set_precision("fp32")
-
-
-# ---- k_mlp16's per-CU chunk queue (one 12-wave workgroup per CU, chunks claimed through LDS)
-
-CUQ = 1 << 12
-
-
-@pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_mlp_cu_queue_equals_grid_stride(rend, nets, prec):
-    """Every point evaluated exactly once by the CU-queue launch (ragged sizes, fewer chunks than
-    CUs, a 4-input network below), the same values as the grid-stride launch (bit 12), and repeated
-    launches stay right.  (Bit 12 selects the queue.)"""
-    dims, K, B = nets["car_1"]
-    rend.load_mlp(dims, K, B).set_precision(prec)
-    rng = np.random.default_rng(25)
-    try:
-        for n in (1, 129, 128 * 777 + 5, (1 << 18) + 77, (1 << 20) + 64, 3_000_001):
-            X = rng.uniform(-1.2, 1.2, size=(n, 3)).astype(np.float32)
-            rend.set_debug(0)
-            ref = rend.mlp_forward(X)
-            rend.set_debug(CUQ)
-            for rep in range(3):
-                a = rend.mlp_forward(X)
-                assert np.array_equal(a, ref), (n, rep, int((a != ref).sum()))
-    finally:
-        rend.set_debug(0)
-        rend.set_precision("fp32")
-
-
-# ---- the batched bf16/fp16 tracer with two ray groups per wave (k_trace2) against k_trace
-
-TWO_GROUPS = 1 << 14   # flips the build's default tracer (k_trace) to k_trace2
-
-
-@pytest.mark.parametrize("prec", ["bf16", "fp16"])
-@pytest.mark.parametrize("geom,size,frames", [("car_1", 512, 6), ("plane_2", 384, 32), ("plane_1", 200, 3)])
-def test_two_group_tracer_frames_identical(rend, chrome, geom, size, frames, prec):
-    """Every pixel of a batch (several sizes, up to 32 frames, poses and frame numbers) identical
-    between the two-group tracer (nr_set_debug bit 14) and the one-group k_trace, and the same
-    ray-step and shaded-ray counts."""
-    rend.load_h5(nr.geometry_path(geom)).set_precision(prec)
-    rend.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
-    cams = [nr.camera(7.0 * (i % 5), 23.0 * i, 2.0) + (i,) for i in range(frames)]
-    try:
-        rend.set_debug(0)
-        a, sa = rend.render_batch(size, size, cams, 128)
-        rend.set_debug(TWO_GROUPS)
-        b, sb = rend.render_batch(size, size, cams, 128)
-        for i, (x, y) in enumerate(zip(a, b)):
-            assert np.array_equal(x, y), (i, int((x != y).sum()))
-        assert sa["ray_steps"] == sb["ray_steps"] and sa["rays_shaded"] == sb["rays_shaded"], (sa, sb)
-    finally:
-        rend.set_debug(0)
-        rend.set_precision("fp32")
-
-
-def test_two_group_tracer_animation_and_facing(rend):
-    """A 4-input network (the frame number rides in the 128-point MLP's inputs) with facing-ratio
-    colouring (the ray direction regenerated from the pixel), batched: identical to k_trace."""
-    rng = np.random.default_rng(26)
-    dims = [4] + [32] * 8 + [1]
-    K = [(rng.standard_normal((dims[i], dims[i + 1])) / np.sqrt(dims[i])).astype(np.float32) for i in range(9)]
-    B = [(rng.standard_normal(dims[i + 1]) * 0.05).astype(np.float32) for i in range(9)]
-    B[-1][:] = 0.2
-    rend.load_mlp(dims, K, B).set_precision("bf16")
-    rend.set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
-    cams = [nr.camera(0.0, 11.0 * i, 2.0) + (5 * i,) for i in range(5)]
-    try:
-        rend.set_debug(0)
-        a, sa = rend.render_batch(256, 192, cams, 96)
-        rend.set_debug(TWO_GROUPS)
-        b, sb = rend.render_batch(256, 192, cams, 96)
-        for i, (x, y) in enumerate(zip(a, b)):
-            assert np.array_equal(x, y), (i, int((x != y).sum()))
-        assert sa["ray_steps"] == sb["ray_steps"]
-    finally:
-        rend.set_debug(0)
-        rend.set_static(nr.NR_COLOR_MATCAP, 3).set_precision("fp32")

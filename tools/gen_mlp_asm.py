@@ -276,14 +276,11 @@ def main():
         "// v[64+8t+4s:+3]; in: the input layer's B operands in k-step 0's slot; out: the ReLU'd final",
         "// operands), A operands v96-v111 and biases v112-v143 (two buffers each); %[va] = LDS byte",
         "// address of the A operands + 16 lane, %[vb] = of the biases + 64 (lane >> 5).",
-        "// NR_HID7X2_*: the same for two tiles (the tracer's 64 points): accumulators v0-v31, B operands",
-        "// v32-v47, A operands v48-v63, biases v64-v95.",
         "#pragma once",
         "",
     ]
     for name, prec, clamp, nt in (("NR_HID7_BF16_CLAMP", "bf16", True, 4), ("NR_HID7_BF16_MAX", "bf16", False, 4),
-                                  ("NR_HID7_F16_MAX", "fp16", False, 4), ("NR_HID7X2_BF16_CLAMP", "bf16", True, 2),
-                                  ("NR_HID7X2_BF16_MAX", "bf16", False, 2), ("NR_HID7X2_F16_MAX", "fp16", False, 2)):
+                                  ("NR_HID7_F16_MAX", "fp16", False, 4)):
         st = build(prec, clamp, nt)
         nm = sum(1 for x in st.ins if x[1] == "mfma")
         nv = sum(1 for x in st.ins if x[1] == "valu")

@@ -3,7 +3,7 @@
 # (profile_round.sh) and the MLP microbenchmark over every precision.  Each GPU step has
 # its own time limit and the steps are chained, so the first failure ends the session.
 # usage (GPU box, repo root): bash tools/gpu_session.sh TAG [steps...]
-#   steps: smoke tests prof mlp cfg pmc_bf16 pmc_fp16 pmc_x3 march bench   (default: smoke tests prof mlp)
+#   steps: smoke tests prof mlp cfg pmc_bf16 pmc_fp16 pmc_x3 march bench peak   (default: smoke tests prof mlp)
 #   env: PYTEST_EXTRA (extra pytest arguments, no spaces inside one), PYTEST_K (a -k expression),
 #        BENCH_ARGS
 set -o pipefail
@@ -24,6 +24,7 @@ for s in $STEPS; do
     pmc_x3) timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_x3_$TAG fp32x3 12 > $O/pmc_x3_$TAG.txt 2>&1 ;;
     march) timeout -k 10 400 bash tools/march_traffic.sh $O/march_$TAG 8 > $O/march_$TAG.json 2> $O/march_$TAG.err ;;
     bench) timeout -k 10 300 python -u bench.py $BENCH_ARGS > $O/bench_$TAG.json 2> $O/bench_$TAG.err ;;
+    peak) timeout -k 10 200 tools/bin/mfma_peak_random > $O/peak_$TAG.txt 2>&1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
     esac
     rc=$?
