@@ -6,7 +6,7 @@ Compute lives in ``lib/libnr.so`` (HIP, gfx950) behind the C ABI of
 """
 import os
 
-from ._lib import LIB_PATH, NR_PRECISION, NR_SCENE, NR_SCHEDULE, NRError, lib  # noqa: F401
+from ._lib import LIB_PATH, NR_ENDGAME_DEFAULT, NR_PRECISION, NR_SCENE, NR_SCHEDULE, NRError, lib  # noqa: F401
 from .renderer import (NR_COLOR_FACING, NR_COLOR_MATCAP, Group, Renderer, assemble_shards, camera,  # noqa: F401
                        load_png, pack_x3, read_keras_h5, save_png, save_ppm, shard_rows, batch_frames_per_launch)
 

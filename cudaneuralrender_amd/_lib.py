@@ -17,6 +17,7 @@ NR_SCENE = {"v1": 0, "tanh": 1, "subtract": 2, "cylinders": 3, "displace": 4, "r
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
 NR_SCHEDULE = {"persistent": 0, "wavefront": 1, "layered": 2}
+NR_ENDGAME_DEFAULT = 0.001  # include/neural_render.h: the bf16/fp16 endgame threshold by default
 
 # every symbol include/neural_render.h declares
 EXPORTS = [
@@ -30,6 +31,7 @@ EXPORTS = [
     "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
     "nr_h5_dims", "nr_h5_read_f32",
     "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch", "nr_pack_x3",
+    "nr_set_endgame",
 ]
 
 
@@ -42,6 +44,7 @@ class NRStats(ctypes.Structure):
         ("iterations", ctypes.c_int32),
         ("launches", ctypes.c_int32),
         ("ms_total", ctypes.c_float),
+        ("endgame_evals", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -143,6 +146,7 @@ def lib():
         "nr_set_poll_interval": (I, [P, I]),
         "nr_set_schedule": (I, [P, I]),
         "nr_set_debug": (I, [P, I]),
+        "nr_set_endgame": (I, [P, F]),
         "nr_set_occupancy": (I, [P, I]),
         "nr_set_age_hold": (I, [P, I, I]),
         "nr_set_pixel_spread": (I, [P, I]),

@@ -45,6 +45,7 @@ struct nr_ctx {
     uint16_t *d_x3lp = nullptr;  // bf16/fp16: the fp32x3 pack for the normals (MlpArgs::x3n)
     float *d_x3fl = nullptr;
     bool fp32_normals = false;   // nr_set_debug bit 15: the bf16/fp16 tracers' normals in fp32 (A/B)
+    float eg_tau = NR_ENDGAME_DEFAULT;  // nr_set_endgame: bf16/fp16 persistent renders' fp32x3 endgame
     float *d_lpf16 = nullptr;
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
@@ -337,6 +338,14 @@ int num_cus(int dev) {
 
 
 int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
+
+// The endgame's threshold for a persistent render (TraceArgs::eg_tau): nr_set_endgame's, for the
+// bf16/fp16 tracers with fp32x3 normals (the fine passes use their fp32x3 pack) and iteration
+// counts that fit the fine queue's 24 bits; 0 otherwise (the pure 16-bit march)
+static float endgame_tau(const nr_ctx *c, int max_steps) {
+    const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
+    return lowp && c->mlp16.x3n && max_steps < (1 << 24) ? c->eg_tau : 0.0f;
+}
 
 // Persistent-tracer workgroups per CU for a launch of `total` pixels over `nframes` frames
 // (profiles/r2_occupancy.txt, r2_single_bpc.txt, r2_lowp_occ.txt):
@@ -888,7 +897,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
             rc = nr_render_shard(c, frames[i].out, W, H, band, nshards, shard, max_steps, loc, stats ? &st : nullptr);
             tot.ray_steps += st.ray_steps; tot.shade_evals += st.shade_evals; tot.rays_hit += st.rays_hit;
             tot.rays_shaded += st.rays_shaded; tot.iterations = std::max(tot.iterations, st.iterations);
-            tot.launches += st.launches; tot.ms_total += st.ms_total;
+            tot.launches += st.launches; tot.ms_total += st.ms_total; tot.endgame_evals += st.endgame_evals;
         }
         memcpy(c->inv_view, iv, sizeof iv);
         memcpy(c->normal, nm, sizeof nm);
@@ -920,7 +929,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     A.max_steps = max_steps; A.scene = c->scene; A.frame = 0; A.color_type = c->color_type;
     A.matcap = c->d_matcap; A.mw = c->mw; A.mh = c->mh;
     set_recips(A);
-    const size_t tr_bytes = NR_MAX_QUEUES * 128 + 4 * 8;
+    const size_t tr_bytes = NR_MAX_QUEUES * 128 + 8 * 8;
     if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
     TraceArgs T{};
     T.pix_ctr = c->d_tr;
@@ -957,6 +966,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // (1024^2 x 32 frames 1.866 -> 1.825 ms/frame, one 8-way shard x 8 frames 0.367 ->
         // 0.334; profiles/r2_ab_experiments.txt (10)).  Debug bit 10: frame-major (A/B).
         T.interleave = !((c->debug >> 10) & 1);
+        T.eg_tau = endgame_tau(c, max_steps);
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,
@@ -989,10 +999,11 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (c->profiling) c->prof_renders += nframes;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     if (stats) {
-        unsigned long long hs[4];
+        unsigned long long hs[5];
         HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         st.ray_steps = hs[0];
+        st.endgame_evals = hs[4];
         st.rays_hit = hs[1];
         st.iterations = (int32_t)hs[2];
         st.rays_shaded = hs[3];
@@ -1076,7 +1087,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
     if (c->schedule == NR_SCHED_PERSISTENT) {
         // 8 shard counters on their own 128-byte lines, then 4 x u64 stats
         // (a second set for the cost probe)
-        const size_t tr_bytes = NR_MAX_QUEUES * 128 + 4 * 8;
+        const size_t tr_bytes = NR_MAX_QUEUES * 128 + 8 * 8;
         if (!c->d_tr) HIPCHK(c, hipMalloc(&c->d_tr, 2 * tr_bytes));
         TraceArgs T{};
         T.pix_ctr = c->d_tr;
@@ -1089,6 +1100,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.hold_prio = c->hold_prio & 3;
         T.hold_refill = c->hold_prio >= 4;
         T.itmap = (c->debug & 8) != 0;
+        T.eg_tau = endgame_tau(c, max_steps);
         {
             const int sp = spread_for(c, 1, npix);
             T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;
@@ -1152,10 +1164,11 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         HIPCHK(c, hipEventRecord(c->ev1, s));
         if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
         if (stats) {
-            unsigned long long hs[4];
+            unsigned long long hs[5];
             HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             st.ray_steps = hs[0];
+            st.endgame_evals = hs[4];
             st.rays_hit = hs[1];
             st.iterations = (int32_t)hs[2];
             st.rays_shaded = hs[3];
@@ -1407,6 +1420,13 @@ int nr_set_wave_rays(nr_ctx *c, int rays) {
 int nr_set_occupancy(nr_ctx *c, int blocks_per_cu) {
     if (!c || blocks_per_cu < 0 || blocks_per_cu > 16) return set_err(c, NR_E_INVALID, "nr_set_occupancy: bad arguments");
     c->blocks_per_cu = blocks_per_cu;
+    return NR_OK;
+}
+
+int nr_set_endgame(nr_ctx *c, float tau) {
+    if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
+    if (!(tau >= 0.0f) || tau > 1e30f) return set_err(c, NR_E_INVALID, "nr_set_endgame: tau must be finite and >= 0");
+    c->eg_tau = tau;
     return NR_OK;
 }
 

@@ -181,6 +181,7 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             t.iterations = std::max(t.iterations, st[r].iterations);
             t.launches += st[r].launches;
             t.ms_total = std::max(t.ms_total, st[r].ms_total);
+            t.endgame_evals += st[r].endgame_evals;
         }
         *stats = t;
     }

@@ -92,7 +92,8 @@ constexpr int NR_MAX_BATCH = 32;
 struct TraceArgs {
     uint32_t *pix_ctr;          // 2^nq_shift pixel-queue shard counters, one per 128-byte line (stride 32)
     int nq_shift;
-    unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded
+    unsigned long long *stats;  // [0] ray-steps, [1] rays hit, [2] max iterations, [3] rays shaded,
+                                // [4] fp32x3 march evaluations (the endgame)
     unsigned long long *stamps; // diagnostics (nr_set_debug): per wave {start, queue drained, end, ray-steps}
     // pixel queue over 8x8 pixel blocks of the shard image, dispensed in `order`
     // (NULL = raster order); bcost (may be NULL) receives each block's max ray iterations
@@ -116,6 +117,8 @@ struct TraceArgs {
     int interleave;             // batched: 64-position queue chunks dealt to the frames in turn
                                 // (all frames progress together) instead of frame-major
     double inv_nframes;         // 1 / nframes for udiv_r
+    float eg_tau;               // bf16/fp16 with an fp32x3 pack: the endgame's switch threshold (0 = off;
+                                // k_trace's EG instances, nr_set_endgame)
 };
 
 int dense_lds_bytes(int in, int out);

@@ -181,8 +181,21 @@ __device__ __forceinline__ void set_priority(int prio) {
 #define NR_TRACE_BPC_X3 3
 #endif
 // NX3: the bf16/fp16 instances whose normals are fp32x3 (MlpArgs::x3n; mlp16_x3_normal).
-template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false>
-__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
+// EG: the bf16/fp16 instances with the fp32x3 endgame (TraceArgs::eg_tau > 0, round 5): a marching
+// ray whose 16-bit MLP output falls below eg_tau leaves its lane for the wave's fine queue in LDS
+// without taking the step; whenever the queue holds a full 32-point tile (or the pixel queue is
+// drained) the wave takes up to 64 queued rays through a fine pass -- the fp32x3 MLP on their
+// points (mlp16_x3_normal's per-point rule: the split within the x3 pack's bounds, the fp32 MLP
+// outside), the scene and singleMarch's step -- and returns the survivors to the queue.  So the
+// switch iteration's step, the convergence test (:474), the background test and every later step
+// of the ray are decided in fp32x3, on full tiles.  Oracle: nr_oracle.c or_set_endgame.
+// (3 workgroups per CU: the fine queue's 13 KB of LDS leaves room for no more)
+#ifndef NR_TRACE_BPC_EG
+#define NR_TRACE_BPC_EG 3
+#endif
+template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false>
+__global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
+                                  : PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                   : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
                                   : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
@@ -221,6 +234,14 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // each lane's marching ray {d.xyz, pixel} (DLDS): 4 KB per workgroup
     constexpr bool DLDS = DENSE && NR_RAY_D_LDS;
     __shared__ float4 ray_dp[DLDS ? 4 : 1][DLDS ? 64 : 1];
+    // EG: per wave the fine queue {p.xyz, tfar}, {d.xyz, pixel}, iteration | frame << 24: a pass
+    // leaves fewer than 32 rays (or none), one iteration adds at most 64
+    static_assert(!EG || (DLDS && NX3 && (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16)), "EG instances");
+    constexpr int FQ = EG ? 32 - 1 + 64 : 1;
+    __shared__ float4 fq_p[EG ? 4 : 1][FQ], fq_d[EG ? 4 : 1][FQ];
+    __shared__ uint32_t fq_i[EG ? 4 : 1][FQ];
+    int nfq = 0;        // rays in the wave's fine queue (EG)
+    uint32_t nfine = 0;  // fp32x3 march evaluations (EG)
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -276,6 +297,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         pend = __builtin_amdgcn_readfirstlane((int)pend) != 0;
         rb_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_n);
         rb_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_head);
+        if constexpr (EG) nfq = __builtin_amdgcn_readfirstlane(nfq);
         // ---- refill free slots from the pixel queue
         if ((!qempty || (DENSE && rb_n > 0)) && !(hold && !T.hold_refill)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
@@ -530,7 +552,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         uint64_t lm = __ballot(it >= 0);
         constexpr int SHR = PREC == NR_PRECISION_FP32 ? 16 : NR_SHADE_RAYS_LOWP;  // rays per shading pass
-        while (nstash >= SHR || (drained && nstash > 0 && !lm)) {
+        bool fpass = false;  // EG: a fine pass ran in this iteration
+        while (true) {
+        while (nstash >= SHR || (drained && nstash > 0 && !lm && nfq == 0)) {
             const int nb = min(SHR, nstash);
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
@@ -570,9 +594,91 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             nconv += (uint32_t)nb;
             nstash -= nb;
         }
+        // ---- EG: a fine pass over up to 64 rays of the fine queue (two 32-point tiles) whenever
+        // it holds a full tile -- repeated while it does -- and, once the pixel queue is drained,
+        // one per iteration (all of them when no coarse ray is left).  The stash holds fewer than
+        // SHR rays here and a pass adds at most 64 converged ones.
+        if constexpr (EG) {
+            if (nfq >= 32 || (drained && nfq > 0 && (!lm || !fpass))) {
+                fpass = true;
+                const int nb = min(64, nfq);
+                const int base = nfq - nb;
+                const bool act = lane < nb;
+                const int e = base + (act ? lane : 0);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const float4 qp = fq_p[wid][e], qd = fq_d[wid][e];
+                const uint32_t qi = fq_i[wid][e];
+                F3 fp = mk3(qp.x, qp.y, qp.z);
+                float ftf = qp.w;
+                const uint32_t fpix = __float_as_uint(qd.w);
+                int fit = (int)(qi & 0xffffffu);
+                const int ff = BATCH ? (int)(qi >> 24) : 0;
+                // the fp32x3 pack's address made opaque, as in the shading pass
+                int zx = 0;
+                asm volatile("" : "+s"(zx));
+                const float fsdf = mlp16_x3_normal(M, S.s32, M.x3lp + zx, M.x3fl + zx, fr_of(ff), fp.x, fp.y, fp.z,
+                                                   nb > 32 ? 0xfu : 0x3u);
+                nfine += (uint32_t)nb;
+                nsteps += (uint32_t)nb;
+                bool fconv = false, keep = false;
+                if (act) {
+                    // singleMarch (:416-477) on the fp32x3 value, as the coarse step below
+                    const float ts = scene_sdf(fp, fsdf, A.scene, zoff_of(ff));
+                    ftf -= ts;
+                    int used = 0;
+                    if (ftf <= 0) {
+                        put(ff, fpix, 0u);
+                        used = fit + 1;
+                    } else {
+                        fp = add3(fp, mul3s(mk3(qd.x, qd.y, qd.z), ts));
+                        if (ts < MARCHING_EPSILON) {
+                            if (fit + 1 < A.max_steps) {
+                                fconv = true;
+                                used = fit + 2;
+                            } else {
+                                put(ff, fpix, 0u);
+                                used = fit + 1;
+                            }
+                        } else if (++fit >= A.max_steps) {
+                            put(ff, fpix, 0u);
+                            used = A.max_steps;
+                        }
+                    }
+                    if (used) {
+                        maxit = max(maxit, used);
+                        if (T.itmap) put(ff, fpix, (uint32_t)used);
+                        if (T.bcost) {
+                            const int yy = (int)(fpix / (uint32_t)A.W), xx = (int)(fpix - (uint32_t)yy * A.W);
+                            atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
+                        }
+                    } else {
+                        keep = true;
+                    }
+                }
+                // survivors back to the queue (positions [base, base + survivors)), converged rays
+                // to the stash
+                const uint64_t km = __ballot(keep), cm = __ballot(fconv);
+                if (keep) {
+                    const int slot = base + (int)rank_below(km);
+                    fq_p[wid][slot] = make_float4(fp.x, fp.y, fp.z, ftf);
+                    fq_d[wid][slot] = qd;
+                    fq_i[wid][slot] = (uint32_t)fit | ((uint32_t)ff << 24);
+                }
+                if (fconv) {
+                    const int slot = nstash + (int)rank_below(cm);
+                    stash[wid][slot] = make_float4(fp.x, fp.y, fp.z, __uint_as_float(fpix));
+                    if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)ff;
+                }
+                nstash += (int)__popcll(cm);
+                nfq = base + (int)__popcll(km);
+                continue;
+            }
+        }
+        break;
+        }
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         if (!lm) {
-            if (drained && nstash == 0) break;
+            if (drained && nstash == 0 && nfq == 0) break;
             continue;
         }
         uint32_t tmask = tiles_of(lm);
@@ -615,9 +721,29 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             if (lane == 0) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
             nsteps = 0;
         }
+        if (EG && nfine >= (1u << 30)) {
+            if (lane == 0) atomicAdd(T.stats + 4, (unsigned long long)nfine);
+            nfine = 0;
+        }
         ++wit;
         wit_tail += drained ? 1u : 0u;
         bool conv = false;
+        if constexpr (EG) {
+            // the endgame's switch: the ray goes to the fine queue without taking the step (the
+            // fine pass re-evaluates this point in fp32x3); its lane is free for a new ray
+            const bool hand = it >= 0 && sdf < T.eg_tau;
+            const uint64_t hm = __ballot(hand);
+            if (hm) {
+                if (hand) {
+                    const int slot = nfq + (int)rank_below(hm);
+                    fq_p[wid][slot] = make_float4(p.x, p.y, p.z, tfar);
+                    fq_d[wid][slot] = ray_dp[wid][lane];
+                    fq_i[wid][slot] = (uint32_t)it | ((uint32_t)rf << 24);
+                    it = -1;
+                }
+                nfq += (int)__popcll(hm);
+            }
+        }
         if (it >= 0) {
             const float ts = scene_sdf(p, sdf, A.scene, zoff_of(rf));
             if constexpr (timing) {
@@ -689,6 +815,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         if (nhit) atomicAdd(T.stats + 1, (unsigned long long)nhit);
         if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
         if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
+        if (EG && nfine) atomicAdd(T.stats + 4, (unsigned long long)nfine);
     }
 }
 
@@ -954,6 +1081,19 @@ static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const Tr
                                  hipStream_t st) {
     constexpr bool LOWP = PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16;
     if constexpr (LOWP && !PROBE) {
+        if constexpr (!STAMPS) {
+            if (M.x3n && T.eg_tau > 0.0f) {
+                // the fine queue's LDS leaves room for NR_TRACE_BPC_EG workgroups per CU: a grid of
+                // more would queue workgroups behind the resident ones
+                int dev = 0, cus = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                    return hipErrorInvalidDevice;
+                const int g = std::max(1, std::min(grid, NR_TRACE_BPC_EG * cus));
+                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(g), dim3(256), sm, st, A, M, T);
+                return hipGetLastError();
+            }
+        }
         if (M.x3n) {
             hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true>), dim3(grid), dim3(256), sm, st, A, M, T);
             return hipGetLastError();

@@ -271,6 +271,12 @@ class Renderer:
         self._chk(self._L.nr_set_debug(self._ctx, int(flags)))
         return self
 
+    def set_endgame(self, tau):
+        """nr_set_endgame: bf16/fp16 rays whose 16-bit MLP output falls below tau finish their
+        march in fp32x3 (default 0.001; 0 = the pure 16-bit march)."""
+        self._chk(self._L.nr_set_endgame(self._ctx, float(tau)))
+        return self
+
     def debug_stamps(self):
         """Per-wave stamps of the last k_trace: {start, queue drained, end (100 MHz ticks),
         iterations after drain << 32 | iterations, shader-clock cycles in refill, shading,

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define NR_ABI_VERSION 1
+#define NR_ABI_VERSION 2   /* 2: nr_stats.endgame_evals, nr_set_endgame (round 5) */
 
 /* status codes */
 #define NR_OK 0
@@ -77,6 +77,8 @@ typedef struct nr_stats {
     int32_t iterations;      /* march iterations that had live rays (reference host-loop count) */
     int32_t launches;        /* kernel launches issued */
     float ms_total;          /* device time of the render, HIP events */
+    uint64_t endgame_evals;  /* bf16/fp16 with the endgame (nr_set_endgame): the march evaluations
+                                in fp32x3, included in ray_steps */
 } nr_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -239,6 +241,17 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * samples of every coloured ray) by the fp32 MLP instead of the fp32x3 split (A/B; the frames'
  * march is the same, their shading moves by the two forms' rounding). */
 int nr_set_debug(nr_ctx *ctx, int flags);
+/* The reduced-precision endgame (bf16 / fp16, persistent schedule; round 5): a marching ray whose
+ * 16-bit MLP output falls below tau (a surface is near) re-evaluates that point in fp32x3 and
+ * takes every later step of its march in fp32x3, so the convergence test (tstep < 1e-6,
+ * volumeRender_kernel.cu:474), the background test and the hit point are decided at fp32-class
+ * precision while the bulk of the march stays 16-bit.  Default NR_ENDGAME_DEFAULT; 0 = the pure
+ * 16-bit march.  It needs the network's fp32x3 pack (the 7-hidden-layer [3|4, 32..., 1] shape whose
+ * scales fit, as for the fp32x3 normals) and is off with nr_set_debug bit 15 (fp32 normals); the
+ * wavefront and layered schedules march in pure 16-bit.  nr_stats.endgame_evals counts the fp32x3
+ * evaluations. */
+#define NR_ENDGAME_DEFAULT 0.001f
+int nr_set_endgame(nr_ctx *ctx, float tau);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next
  * launch of the same size/shard dispenses blocks longest-first (pixels are unaffected --

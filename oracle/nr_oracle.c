@@ -1196,6 +1196,18 @@ int or_render(int nlayers, const int *dims, const float *params,
                         matcap, mw, mh, W, H, max_steps, out, stats, nthreads, 0, 0, H);
 }
 
+/* The reduced-precision endgame (libnr nr_set_endgame; round 5): with tau > 0, a precision-1/2 ray
+ * whose 16-bit MLP output at its current point is below tau re-evaluates that point in fp32x3
+ * (precision 4) in the same iteration -- the step, the convergence test (:474) and the
+ * background test use the fp32x3 value -- and takes every later iteration of its march in
+ * fp32x3 (the switch is one-way).  g_eg_evals counts the fp32x3 march evaluations of the last
+ * render (the switch iteration's 16-bit evaluation is counted as a ray-step, its re-evaluation
+ * here). */
+static float g_eg_tau = 0.0f;
+static long long g_eg_evals = 0;
+void or_set_endgame(float tau) { g_eg_tau = tau; }
+long long or_endgame_evals(void) { return g_eg_evals; }
+
 int or_render_ex(int nlayers, const int *dims, const float *params,
                  const float *inv_view, const float *normal, int frame,
                  int color_type, int num_inputs, int scene,
@@ -1229,8 +1241,14 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
     float *batch = (float *)calloc((size_t)npix * num_inputs * COLOR_MASK_VAL, sizeof(float));
     float *sdf = (float *)calloc((size_t)npix * COLOR_MASK_VAL, sizeof(float));
     unsigned char *bprec = (unsigned char *)calloc((size_t)npix * COLOR_MASK_VAL, 1);
-    if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf || !bprec) {
+    /* the endgame: fine[i] = pixel i marches in fp32x3; redo[i] = re-evaluate it this iteration */
+    const int eg = (precision == 1 || precision == 2) && g_eg_tau > 0.0f && g_x3.a;
+    unsigned char *fine = (unsigned char *)calloc(npix, 1);
+    long *redo = (long *)calloc(npix, sizeof(long));
+    g_eg_evals = 0;
+    if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf || !bprec || !fine || !redo) {
         free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf); free(bprec);
+        free(fine); free(redo);
         if (qp) lowp_free(&q);
         return -5;
     }
@@ -1280,7 +1298,8 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
             if (mv == 1) {
                 batch[bi] = points[3 * i]; batch[bi + 1] = points[3 * i + 1]; batch[bi + 2] = points[3 * i + 2];
                 if (ni == 4) batch[bi + 3] = (float)frame;
-                bprec[idmap[i]] = (unsigned char)precision;
+                bprec[idmap[i]] = fine[i] ? 4 : (unsigned char)precision;
+                if (fine[i]) g_eg_evals++;
             } else {
                 for (unsigned q = 0; q < mv; ++q) {
                     size_t o = bi + (size_t)q * ni;
@@ -1296,6 +1315,30 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
         long long shaded = 0;
         /* nn.forward(batch) :661 */
         mlp_forward_mixed(&m, qp, batch, batchSize, ni, sdf, bprec, nthreads);
+        /* the endgame's switch: a 16-bit ray whose MLP output is below tau is re-evaluated in
+         * fp32x3 before it takes the step */
+        long nredo = 0;
+        if (eg) {
+            for (long id = 0; id < npix; ++id)
+                if (mask[id] == 1 && !fine[id] && sdf[idmap[id]] < g_eg_tau) {
+                    fine[id] = 1;
+                    redo[nredo++] = id;
+                }
+            if (nredo) {
+                float *xb = (float *)malloc(sizeof(float) * (size_t)nredo * ni);
+                float *yb = (float *)malloc(sizeof(float) * (size_t)nredo);
+                unsigned char *pb = (unsigned char *)malloc((size_t)nredo);
+                for (long r = 0; r < nredo; ++r) {
+                    memcpy(xb + (size_t)r * ni, batch + (size_t)idmap[redo[r]] * ni, sizeof(float) * (size_t)ni);
+                    pb[r] = 4;
+                }
+                mlp_forward_mixed(&m, qp, xb, nredo, ni, yb, pb, nthreads);
+                for (long r = 0; r < nredo; ++r) sdf[idmap[redo[r]]] = yb[r];
+                g_eg_evals += nredo;
+                st[0] += nredo;   /* a ray-step is a march evaluation: the re-evaluation is one */
+                free(xb); free(yb); free(pb);
+            }
+        }
         /* singleMarch :416-477 */
 #ifdef _OPENMP
 #pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : omp_get_max_threads()) reduction(+:shaded)
@@ -1333,6 +1376,7 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
     }
     if (stats) memcpy(stats, st, sizeof st);
     free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf); free(bprec);
+    free(fine); free(redo);
     if (qp) lowp_free(&q);
     return 0;
 }

@@ -63,6 +63,10 @@ def lib():
         L.or_trace_mfma.argtypes = [P, ctypes.c_long]
         L.or_trace_count.restype = ctypes.c_long
         L.or_trace_count.argtypes = []
+        L.or_set_endgame.restype = None
+        L.or_set_endgame.argtypes = [ctypes.c_float]
+        L.or_endgame_evals.restype = ctypes.c_longlong
+        L.or_endgame_evals.argtypes = []
         _lib = L
     return _lib
 
@@ -109,10 +113,13 @@ class OracleNet:
         return Y
 
     def render(self, W, H, inv_view, normal, frame=0, color_type=0, num_inputs=3, scene=0, matcap=None,
-               max_steps=6000, nthreads=0, precision=0, rows=None):
+               max_steps=6000, nthreads=0, precision=0, rows=None, endgame=0.0):
         """precision 1/2: the GPU's bf16/fp16 MLP arithmetic (nr_oracle.c mlp_point_gpu_lowp) for
         the marching points; the normals in fp32x3 when the net holds an x3 pack (as the bf16/fp16
-        tracers compute them), else fp32.  rows=(y0, y1): render only those rows of the frame."""
+        tracers compute them), else fp32.  rows=(y0, y1): render only those rows of the frame.
+        endgame > 0 (precision 1/2, a net with an x3 pack): a ray whose 16-bit MLP output falls below
+        it is re-evaluated and marched from then on in fp32x3 (nr_oracle.c or_set_endgame); the
+        stats then carry "endgame_evals", the fp32x3 march evaluations."""
         y0, y1 = rows if rows is not None else (0, H)
         out = np.zeros((y1 - y0, W), np.uint32)
         stats = np.zeros(5, np.int64)
@@ -124,12 +131,17 @@ class OracleNet:
         else:
             mc, mp, mw, mh = None, None, 0, 0
         self._x3_on()
+        lib().or_set_endgame(float(endgame))
         rc = lib().or_render_ex(self.nlayers, self.dims.ctypes.data, self.params.ctypes.data, iv.ctypes.data,
                                 nm.ctypes.data, frame, color_type, num_inputs, scene, mp, mw, mh, W, H, max_steps,
                                 out.ctypes.data, stats.ctypes.data, nthreads, precision, y0, y1)
         assert rc == 0, rc
         keys = ["ray_steps", "shade_evals", "iterations", "rays_hit", "rays_shaded"]
-        return out, dict(zip(keys, (int(v) for v in stats)))
+        st = dict(zip(keys, (int(v) for v in stats)))
+        if endgame > 0:
+            st["endgame_evals"] = int(lib().or_endgame_evals())
+        lib().or_set_endgame(0.0)
+        return out, st
 
 
 def set_mfma_model(model, w=26):

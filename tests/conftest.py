@@ -62,3 +62,27 @@ def compare_frames(gpu, ref):
             "iou": float(both.sum() / max((fg | fr).sum(), 1)),
             "mean_abs": [round(float(v), 4) for v in (d.mean(0) if len(d) else np.zeros(4))],
             "max_abs": [int(v) for v in (d.max(0) if len(d) else np.zeros(4))]}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def pure_16bit(request):
+    """Modules that set PURE_16BIT = True test the pure bf16 / fp16 march (the round-4 contract
+    against the oracle's precision-1/2 restatement, and the schedules against each other): every
+    Renderer they create starts with nr_set_endgame(ctx, 0) instead of the library's default
+    threshold (NR_ENDGAME_DEFAULT; the endgame's own contract: test_gpu_endgame.py,
+    test_gpu_lowp_contract.py)."""
+    if not getattr(request.module, "PURE_16BIT", False):
+        yield
+        return
+    import cudaneuralrender_amd as nr
+    init = nr.Renderer.__init__
+
+    def init_pure(self, *a, **kw):
+        init(self, *a, **kw)
+        self.set_endgame(0.0)
+
+    nr.Renderer.__init__ = init_pure
+    try:
+        yield
+    finally:
+        nr.Renderer.__init__ = init

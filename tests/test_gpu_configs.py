@@ -14,6 +14,7 @@ import cudaneuralrender_amd as nr
 import oracle
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 NTHREADS = min(16, os.cpu_count() or 1)
 
 

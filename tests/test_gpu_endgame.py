@@ -1,0 +1,175 @@
+"""The reduced-precision endgame (round 5; nr_set_endgame, k_trace's EG instances):
+a bf16 / fp16 ray whose 16-bit MLP output falls below tau re-evaluates that point in fp32x3 and
+takes every later step of its march in fp32x3 (the per-point rule of the fp32x3 normals: the split
+within the x3 pack's input bounds, the fp32 MLP outside), so the convergence test
+(volumeRender_kernel.cu:474 `tstep < 1e-6`), the background test and the hit point are decided at
+fp32-class precision while the bulk stays 16-bit.
+
+Contract: BIT-EXACT against the oracle's restatement (oracle/nr_oracle.c or_set_endgame: the same
+switch rule over the bit-exact bf16 / fp16 / fp32x3 arithmetic) -- every pixel, the ray-step count
+(every march evaluation, the switch iteration's two included) and the number of fp32x3
+evaluations -- over geometries, cameras, both 16-bit precisions, thresholds, scenes, step caps,
+ragged sizes, batches and a 4-input network with frames on both sides of the x3 pack's frame
+bound.  The quality it buys against the exact-MLP frame is asserted in test_gpu_lowp_contract.py."""
+import numpy as np
+import pytest
+
+import cudaneuralrender_amd as nr
+import oracle
+
+pytestmark = pytest.mark.gpu
+PREC = {"bf16": 1, "fp16": 2}
+
+
+@pytest.fixture(scope="module")
+def chrome():
+    return nr.load_png(nr.matcap_path("Chrome"))
+
+
+def _oracle(geom_or_net, K=None, B=None):
+    if K is None:
+        dims, K, B = nr.read_keras_h5(nr.geometry_path(geom_or_net))
+    else:
+        dims = geom_or_net
+    pack = nr.pack_x3(dims, K, B)
+    assert pack[2], "the network's x3 pack must be valid for the endgame"
+    return oracle.OracleNet(K, B, x3_pack=pack[:2])
+
+
+def _check(img, st, ref, rst):
+    assert (ref != 0).any()
+    assert np.array_equal(img, ref), int((img != ref).sum())
+    assert st["ray_steps"] == rst["ray_steps"], (st, rst)
+    assert st["endgame_evals"] == rst["endgame_evals"] > 0, (st, rst)
+    assert st["rays_shaded"] == rst["rays_shaded"], (st, rst)
+
+
+@pytest.mark.parametrize("geom,prec", [("plane_1", "bf16"), ("car_1", "bf16"), ("plane_3", "fp16"), ("plane_2", "fp16")])
+@pytest.mark.parametrize("tau", [nr.NR_ENDGAME_DEFAULT, 0.02])
+def test_endgame_frames_bitexact(chrome, geom, prec, tau):
+    net = _oracle(geom)
+    for cam in ((0.0, 0.0, 2.0), (25.0, 140.0, 2.6)):
+        iv, nm = nr.camera(*cam)
+        with nr.Renderer(0) as r:
+            r.load_h5(nr.geometry_path(geom)).set_precision(prec).set_endgame(tau)
+            r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+            img, st = r.render(160, 144, 128)
+        ref, rst = net.render(160, 144, iv, nm, color_type=1, matcap=chrome, max_steps=128, nthreads=16,
+                              precision=PREC[prec], endgame=tau)
+        _check(img, st, ref, rst)
+
+
+def test_endgame_default_on_and_off(chrome):
+    """nr_set_endgame(0) is the pure 16-bit march (the round-4 contract); the default threshold
+    is NR_ENDGAME_DEFAULT."""
+    net = _oracle("car_1")
+    iv, nm = nr.camera(10.0, 30.0, 2.2)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("car_1")).set_precision("bf16")
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        dflt, sd = r.render(128, 128, 96)
+        r.set_endgame(0)
+        pure, sp = r.render(128, 128, 96)
+    kw = dict(color_type=1, matcap=chrome, max_steps=96, nthreads=16, precision=1)
+    ref_eg, _ = net.render(128, 128, iv, nm, endgame=nr.NR_ENDGAME_DEFAULT, **kw)
+    ref_pure, rp = net.render(128, 128, iv, nm, **kw)
+    assert np.array_equal(dflt, ref_eg) and sd["endgame_evals"] > 0
+    assert np.array_equal(pure, ref_pure) and sp["endgame_evals"] == 0 and sp["ray_steps"] == rp["ray_steps"]
+    assert not np.array_equal(dflt, pure)
+
+
+@pytest.mark.parametrize("scene", ["tanh", "subtract", "displace"])
+def test_endgame_scenes(chrome, scene):
+    net = _oracle("plane_1")
+    iv, nm = nr.camera(-15.0, 60.0, 2.0)
+    sid = nr.NR_SCENE[scene]
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("plane_1")).set_precision("bf16")
+        r.set_view(iv, nm, 3).set_static(nr.NR_COLOR_FACING, 3).set_scene(scene)
+        img, st = r.render(128, 112, 128)
+    ref, rst = net.render(128, 112, iv, nm, frame=3, color_type=0, scene=sid, max_steps=128, nthreads=16,
+                          precision=1, endgame=nr.NR_ENDGAME_DEFAULT)
+    _check(img, st, ref, rst)
+
+
+@pytest.mark.parametrize("W,H,steps", [(1, 1, 64), (7, 301, 128), (96, 96, 1), (96, 96, 5), (96, 96, 0)])
+def test_endgame_sizes_and_caps(chrome, W, H, steps):
+    net = _oracle("car_1")
+    iv, nm = nr.camera(0.0, 0.0, 2.0) if W > 1 else nr.camera(0.0, 0.0, 0.01)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("car_1")).set_precision("fp16")
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        img, st = r.render(W, H, steps)
+    ref, rst = net.render(W, H, iv, nm, color_type=1, matcap=chrome, max_steps=steps, nthreads=16, precision=2,
+                          endgame=nr.NR_ENDGAME_DEFAULT)
+    assert np.array_equal(img, ref), int((img != ref).sum())
+    assert st["ray_steps"] == rst["ray_steps"] and st["endgame_evals"] == rst.get("endgame_evals", 0)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_endgame_batch_equals_single_frames(chrome, prec):
+    """A batch (every frame's rays share the waves and their fine queues) equals the single-frame
+    renders and the oracle, frame by frame."""
+    net = _oracle("plane_2")
+    cams = [nr.camera(7.0 * i, 41.0 * i, 2.0 + 0.1 * i) + (i,) for i in range(5)]
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("plane_2")).set_precision(prec)
+        r.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        imgs, bst = r.render_batch(144, 128, cams, 128)
+        singles = []
+        for iv, nm, f in cams:
+            r.set_view(iv, nm, f)
+            singles.append(r.render(144, 128, 128))
+    tot_steps = tot_eg = 0
+    for (iv, nm, f), img, (one, st) in zip(cams, imgs, singles):
+        ref, rst = net.render(144, 128, iv, nm, frame=f, color_type=1, matcap=chrome, max_steps=128, nthreads=16,
+                              precision=PREC[prec], endgame=nr.NR_ENDGAME_DEFAULT)
+        assert np.array_equal(img, ref) and np.array_equal(one, ref), (f, int((img != ref).sum()))
+        assert st["ray_steps"] == rst["ray_steps"] and st["endgame_evals"] == rst["endgame_evals"]
+        tot_steps += rst["ray_steps"]
+        tot_eg += rst["endgame_evals"]
+    assert bst["ray_steps"] == tot_steps and bst["endgame_evals"] == tot_eg
+
+
+def test_endgame_four_input_network_frame_bound():
+    """A 4-input network (the frame as 4th input): frames within the x3 pack's frame bound finish
+    in the split, frames beyond it (1500) in the fp32 MLP -- per point, in a batch too."""
+    rng = np.random.default_rng(31)
+    dims = [4] + [32] * 8 + [1]
+    K = [rng.normal(0, 0.3, size=(dims[i], dims[i + 1])).astype(np.float32) for i in range(len(dims) - 1)]
+    K[0][3] *= 0.0005
+    B = [rng.normal(0, 0.05, size=dims[i + 1]).astype(np.float32) for i in range(len(dims) - 1)]
+    B[-1][0] = 0.2
+    net = _oracle(dims, K, B)
+    iv, nm = nr.camera(0.0, 20.0, 2.0)
+    frames = [3, 1500, 1024, 7]
+    with nr.Renderer(0) as r:
+        r.load_mlp(dims, K, B).set_precision("bf16").set_endgame(0.01)
+        r.set_static(nr.NR_COLOR_FACING, 4).set_scene("v1")
+        imgs, _ = r.render_batch(96, 80, [(iv, nm, f) for f in frames], 96)
+    for f, img in zip(frames, imgs):
+        ref, _ = net.render(96, 80, iv, nm, frame=f, color_type=0, num_inputs=4, max_steps=96, nthreads=16,
+                            precision=1, endgame=0.01)
+        assert np.array_equal(img, ref), (f, int((img != ref).sum()))
+    assert any((i != 0).any() for i in imgs)
+
+
+def test_endgame_off_for_fp32_normals_and_other_schedules(chrome):
+    """Bit 15 (fp32 normals) and the wavefront schedule march in pure 16-bit (no fp32x3 pass)."""
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("plane_1")).set_precision("bf16")
+        iv, nm = nr.camera(0.0, 0.0, 2.0)
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        r.set_debug(1 << 15)
+        _, st = r.render(96, 96, 64)
+        assert st["endgame_evals"] == 0
+        r.set_debug(0).set_schedule("wavefront")
+        _, st = r.render(96, 96, 64)
+        assert st["endgame_evals"] == 0
+
+
+def test_endgame_rejects_bad_threshold():
+    with nr.Renderer(0) as r:
+        for bad in (-1.0, float("nan"), float("inf")):
+            with pytest.raises(nr.NRError):
+                r.set_endgame(bad)

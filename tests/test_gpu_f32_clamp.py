@@ -12,6 +12,7 @@ import oracle
 from conftest import GEOMS
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 NO_CLAMP = 1 << 9
 
 

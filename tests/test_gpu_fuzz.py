@@ -15,6 +15,7 @@ import cudaneuralrender_amd as nr
 import oracle
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 SCENES = ["v1", "tanh", "subtract", "cylinders", "displace", "round"]
 
 

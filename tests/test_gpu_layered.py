@@ -21,6 +21,7 @@ import cudaneuralrender_amd as nr
 import oracle
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 
 STATS = ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations")
 

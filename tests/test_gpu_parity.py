@@ -11,6 +11,7 @@ import oracle
 from conftest import GEOMS
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 
 
 @pytest.fixture(scope="module")

@@ -10,6 +10,7 @@ import cudaneuralrender_amd as nr
 from conftest import GEOMS
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 NO_CLAMP = 1 << 9
 NO_STREAM = 1 << 11
 

@@ -10,6 +10,7 @@ import cudaneuralrender_amd as nr
 import oracle
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(REPO, "tools", "bin")
 

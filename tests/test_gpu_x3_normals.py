@@ -18,6 +18,7 @@ import oracle
 from conftest import compare_frames
 
 pytestmark = pytest.mark.gpu
+PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 FP32_NORMALS = 1 << 15
 PREC = {"bf16": 1, "fp16": 2}
 

@@ -27,7 +27,11 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
     assert sorted(_lib.EXPORTS) == syms, "Python binding out of sync with the header"
-    assert L.nr_abi_version() == 1
+    assert L.nr_abi_version() == 2
+    # the ctypes mirror of nr_stats and the header's default endgame threshold
+    txt = open(os.path.join(REPO, "include", "neural_render.h")).read()
+    assert float(re.search(r"#define NR_ENDGAME_DEFAULT ([0-9.]+)f", txt).group(1)) == nr.NR_ENDGAME_DEFAULT
+    assert ctypes.sizeof(_lib.NRStats) == 56 and _lib.NRStats.endgame_evals.offset == 48
 
 
 def test_create_without_gpu_fails_cleanly():
@@ -281,7 +285,7 @@ def test_batched_fp32_tracer_has_no_scratch(tmp_path):
     the ds_bpermute addresses of the quad and lane-group shuffles; mbcnt, DPP quad_perm and
     v_permlane swaps need none.)  The stand-alone MLP's fp32 and bf16 instances stay spill-free."""
     res = kernel_resources(_lib.LIB_PATH, tmp_path)
-    want = {"_ZN2nr7k_traceILi0ELb0ELb0ELb1ELb0EEEvNS_10RenderArgsENS_7MlpArgsENS_9TraceArgsE": 128,
+    want = {"_ZN2nr7k_traceILi0ELb0ELb0ELb1ELb0ELb0EEEvNS_10RenderArgsENS_7MlpArgsENS_9TraceArgsE": 128,
             "_ZN2nr7k_mlp16ILi0ELi3EEEvNS_7MlpArgsEPKfPfi": 512}
     for name, cap in want.items():
         r = res[name]
