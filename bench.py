@@ -93,6 +93,11 @@ def parse():
     ap.add_argument("--no-random-poses", action="store_true",
                     help="skip config.random_poses (profiling passes that average the default-pose launches)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--group", action="store_true",
+                    help="one process drives all N GPUs through the C ABI's nr_group (RCCL gather, "
+                         "NR_GROUP_ASYNC) instead of one torch.distributed rank per GPU")
+    ap.add_argument("--no-group", action="store_true",
+                    help="N > 1 under torch.distributed: skip config.group (rank 0's nr_group child run)")
     a = ap.parse_args()
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
@@ -156,12 +161,25 @@ class RankFailed(RuntimeError):
     """Another rank's render of this batch raised."""
 
 
+_STATUS_GROUP = []
+
+
+def status_group(dist):
+    """A gloo (CPU) process group for the status exchange, created once: a rank whose GPU faulted
+    can still take part in it, where an all-reduce on the RCCL group would need that GPU."""
+    if not _STATUS_GROUP:
+        _STATUS_GROUP.append(dist.new_group(backend="gloo"))
+    return _STATUS_GROUP[0]
+
+
 def checked_step(dist, world, device, fn):
     """Runs fn() -- this rank's render of a batch -- and then, before the batch's gather, lets
-    every rank learn whether any rank's fn raised: one all-reduce (MAX) of a status int.  The
-    failing rank re-raises its own error and the others raise RankFailed, so every rank exits
+    every rank learn whether any rank's fn raised: one all-reduce (MAX) of a status int over a
+    gloo group on the CPU (no device sync; the render itself already waited for its counters).
+    The failing rank re-raises its own error and the others raise RankFailed, so every rank exits
     within seconds instead of blocking in the gather until the collective times out (SURVEY.md
-    section 5: a per-rank status all-reduce before the gather)."""
+    section 5: a per-rank status all-reduce before the gather).  One exchange per batch of up to
+    32 frames: ~0.1 ms of gloo over loopback against ~36 ms per 20-frame batch."""
     err = None
     try:
         fn()
@@ -170,8 +188,8 @@ def checked_step(dist, world, device, fn):
     failed = 1 if err is not None else 0
     if world > 1:
         import torch
-        t = torch.tensor([failed], dtype=torch.int32, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([failed], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=status_group(dist) if device != "cpu" else None)
         failed = int(t.item())
     if err is not None:
         raise err
@@ -193,8 +211,122 @@ def self_launch(a):
     return subprocess.run(cmd, env=env).returncode
 
 
+def main_group(a):
+    """--group: one process, N contexts (GPUs 0..N-1) joined by nr_group (csrc/nr_group.hip, the
+    C-ABI multi-GPU product path: row-band shards rendered in parallel, one RCCL gather per call,
+    the re-interleave on GPU 0), NR_GROUP_ASYNC with up to 32 frames per call, so call k + 1
+    renders while call k's shards travel.  Same JSON contract as the rank path."""
+    import torch
+    import cudaneuralrender_amd as nr
+    n = a.gpus
+    if torch.cuda.device_count() < n:
+        raise SystemExit(f"--group --gpus {n}: only {torch.cuda.device_count()} GPUs visible")
+    size = a.size
+    matcap = nr.load_png(nr.matcap_path("Chrome"))
+    iv, nm = nr.camera(0.0, 0.0, 2.0)
+    geometry = a.geometry or GEOMS[0]
+    rs = []
+    for d in range(n):
+        r = nr.Renderer(d)
+        r.load_h5(nr.geometry_path(geometry)).set_precision(a.precision)
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(matcap)
+        rs.append(r)
+    g = nr.Group(rs, asynchronous=True)
+    nbuf = max(a.steps, a.warmup, 1)
+    frames = torch.zeros(nbuf, size * size, dtype=torch.int32, device="cuda:0")
+    cams = [(iv, nm, 0)]
+    counted = {"ray_steps": 0, "shade_evals": 0}
+
+    def run(k):
+        for i0 in range(0, k, MAX_BATCH):
+            m = min(MAX_BATCH, k - i0)
+            st = g.render_batch_device([frames[i0 + i].data_ptr() for i in range(m)], size, size, cams * m,
+                                       a.max_steps, band=BAND, with_stats=True)
+            counted["ray_steps"] += st["ray_steps"]
+            counted["shade_evals"] += st["shade_evals"]
+
+    def sync_all():
+        g.synchronize()
+        for d in range(n):
+            torch.cuda.synchronize(d)
+
+    run(a.warmup)
+    sync_all()
+    rs[0].prof_collect()
+    rs[0].set_profiling(True)
+    counted["ray_steps"] = counted["shade_evals"] = 0
+    t0 = time.perf_counter()
+    run(a.steps)
+    sync_all()
+    dt = time.perf_counter() - t0
+    rs[0].set_profiling(False)
+    prof = rs[0].prof_collect()
+    ref = torch.from_numpy(rs[0].render(size, size, a.max_steps, with_stats=False).view(np.int32).reshape(-1)).to("cuda:0")
+    parity = all(bool(torch.equal(frames[i], ref)) for i in range(a.steps))
+    launches = max(prof["march_launches"], 1)
+    march_avg_ms = prof["march_ms"] / launches
+    # rank 0's k_trace launches render shard 0: its share of the counted work (1 / n of the rows)
+    achieved = (counted["ray_steps"] + counted["shade_evals"]) / n * FLOP_PER_EVAL / launches / (march_avg_ms * 1e-3) / 1e12 \
+        if march_avg_ms > 0 else 0.0
+    peak = PEAK[a.precision]
+    out = {
+        "metric": "Mray-steps/s at 1024^2, plane_1.h5 (frames/s in config.fps)",
+        "value": round(counted["ray_steps"] / dt / 1e6, 3), "unit": "Mray-steps/s", "n_gpus": n, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32" if a.precision == "fp32" else a.precision,
+        "data": f"synthetic camera (default pose), real bundled weights {geometry}.h5 + Chrome.png",
+        "config": {
+            "workload": f"{geometry} {size}x{size}, {a.max_steps} march steps, {a.precision}, Chrome.png, v1 scene, "
+                        f"default camera (BASELINE configs[1])",
+            "config": a.config, "fps": round(a.steps / dt, 3), "ray_steps_counted": int(counted["ray_steps"]),
+            "parallelism": f"nr_group (one process, C ABI): row-band shards x{n} (band {BAND}), one RCCL gather "
+                           f"per call of <= {MAX_BATCH} frames, NR_GROUP_ASYNC (call k+1 renders while call k's "
+                           f"shards travel), re-interleave on GPU 0",
+            "parity_vs_single_gpu_render": parity, "parity_frames_checked": a.steps,
+        },
+        "roofline": {"bound": "mfma", "kernel": "k_trace (batched instance, GPU 0's shard)",
+                     "achieved": round(achieved, 3), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None, "avg_launch_ms": round(march_avg_ms, 5)},
+        "cpu_baseline": None,
+    }
+    if n == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(size, a.max_steps, a.cpu_threads, geometry, matcap, iv, nm)
+    g.close()
+    for r in rs:
+        r.close()
+    return out
+
+
+def group_child(a):
+    """Rank 0 of an N > 1 rank run: the same workload through nr_group in a child process over all
+    N GPUs (WORLD_SIZE etc. dropped from its environment), its JSON line attached as config.group,
+    bounded by a time limit: the C-ABI multi-GPU path measured on the node the driver runs."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--group", "--gpus", str(a.gpus), "--steps", str(a.steps),
+           "--warmup", str(a.warmup), "--config", a.config, "--precision", a.precision, "--size", str(a.size),
+           "--max-steps", str(a.max_steps), "--no-cpu-baseline"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out after 240 s"}
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}", "stderr_tail": p.stderr[-600:]}
+    d = json.loads(lines[-1])
+    return {k: d[k] for k in ("value", "ms_per_step", "n_gpus")} | {
+        "fps": d["config"]["fps"], "parity_vs_single_gpu_render": d["config"]["parity_vs_single_gpu_render"],
+        "parallelism": d["config"]["parallelism"], "roofline_frac_gpu0": d["roofline"]["frac"]}
+
+
 def main():
     a = parse()
+    if a.group:
+        if "WORLD_SIZE" in os.environ:
+            raise SystemExit("--group runs in one process: start it without torch.distributed.run")
+        print(json.dumps(main_group(a)), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(self_launch(a))
     import torch
@@ -437,6 +569,14 @@ def main():
                 traffic_src = name
         break
 
+    # the C-ABI multi-GPU path (nr_group) over the same N GPUs, in a child of rank 0, after every
+    # timed region; the other ranks wait at the barrier (their contexts stay idle meanwhile)
+    group = None
+    if world > 1 and not a.replicas and not a.no_group:
+        torch.cuda.synchronize()
+        if rank == 0:
+            group = group_child(a)
+        dist.barrier()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -475,6 +615,7 @@ def main():
             "per_rank_value": [round(float(x[1] / x[0] / 1e6), 3) for x in per_rank] if world > 1 else None,
             "geometries": [GEOMS[i % len(GEOMS)] for i in range(world)] if a.replicas else None,
             "fp32x3": x3,
+            "group": group,
             "parity_vs_single_gpu_render": parity,
             "parity_frames_checked": nchecked,
             "shard_ray_steps": {"max": int(rank_steps.max()), "mean": round(float(rank_steps.mean()), 1)}

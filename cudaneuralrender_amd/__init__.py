@@ -8,7 +8,8 @@ import os
 
 from ._lib import LIB_PATH, NR_ENDGAME_DEFAULT, NR_PRECISION, NR_SCENE, NR_SCHEDULE, NRError, lib  # noqa: F401
 from .renderer import (NR_COLOR_FACING, NR_COLOR_MATCAP, Group, Renderer, assemble_shards, camera,  # noqa: F401
-                       load_png, pack_x3, read_keras_h5, save_png, save_ppm, shard_rows, batch_frames_per_launch)
+                       load_png, pack_x3, read_keras_h5, save_png, save_ppm, shard_rows, batch_frames_per_launch,
+                       group_layout)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)

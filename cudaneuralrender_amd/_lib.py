@@ -17,6 +17,7 @@ NR_SCENE = {"v1": 0, "tanh": 1, "subtract": 2, "cylinders": 3, "displace": 4, "r
 NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
 NR_SCHEDULE = {"persistent": 0, "wavefront": 1, "layered": 2}
+NR_GROUP_COPY, NR_GROUP_ASYNC = 1, 2
 NR_ENDGAME_DEFAULT = 0.001  # include/neural_render.h: the bf16/fp16 endgame threshold by default
 
 # every symbol include/neural_render.h declares
@@ -31,7 +32,7 @@ EXPORTS = [
     "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
     "nr_h5_dims", "nr_h5_read_f32",
     "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch", "nr_pack_x3",
-    "nr_set_endgame",
+    "nr_set_endgame", "nr_group_create_ex", "nr_group_synchronize", "nr_group_layout",
 ]
 
 
@@ -118,6 +119,9 @@ def lib():
         "nr_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_group_create": (I, [ctypes.POINTER(P), I, ctypes.POINTER(P)]),
         "nr_group_destroy": (I, [P]),
+        "nr_group_create_ex": (I, [ctypes.POINTER(P), I, I, ctypes.POINTER(P)]),
+        "nr_group_synchronize": (I, [P]),
+        "nr_group_layout": (I, [I, I, I, I, I, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
         "nr_group_size": (I, [P]),
         "nr_group_render_batch": (I, [P, ctypes.POINTER(NRFrame), I, I, I, I, I, I, ctypes.POINTER(NRStats)]),
         "nr_shard_rows": (I, [I, I, I, I]),

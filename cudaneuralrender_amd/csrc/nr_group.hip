@@ -11,9 +11,18 @@
 //     ends the call with its error and no collective is started (a status
 //     exchange before the gather, so no GPU waits in a collective for a rank that failed);
 //   * ONE gather per call over xGMI (ncclGroupStart, every rank's ncclSend to rank 0 and rank 0's
-//     ncclRecv from every rank, ncclGroupEnd) brings all frames' shards to the first GPU;
-//   * one re-interleave launch per frame (nr_assemble_shards) writes the frames there.
-// Rays are independent, so nothing is exchanged while the frames march.
+//     ncclRecv from every rank, ncclGroupEnd) brings all frames' shards to the first GPU, on a
+//     communication stream per GPU, not the render streams;
+//   * one re-interleave launch per frame (launch_assemble) writes the frames there, on the first
+//     GPU's communication stream.
+// The shard and gather buffers are double-buffered (call k uses set k & 1): with NR_GROUP_ASYNC a
+// call returns once its gather and re-interleave are enqueued, so call k + 1's render runs while
+// call k's shards travel; a render into a set waits (device-side, hipStreamWaitEvent) until the
+// transfer of the call before last that used it has read it.  NR_GROUP_COPY moves the shards with
+// hipMemcpyPeerAsync instead of RCCL -- the same layout, offsets and re-interleave with another
+// transport -- and lets several contexts share one GPU, which is how a one-GPU box runs 2- and
+// 3-rank groups (tests/test_gpu_group.py).  Rays are independent, so nothing is exchanged while
+// the frames march.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -23,18 +32,23 @@
 #include <vector>
 
 #include "nr_internal.h"
+#include "nr_kernels.h"
 
 struct nr_group {
     int n = 0;
+    int flags = 0;
     std::vector<nr_ctx *> ctx;
     std::vector<int> dev;
-    std::vector<ncclComm_t> comm;
-    std::vector<uint32_t *> shard;      // per context, on its device: its shards of the call's frames
-    std::vector<size_t> shard_cap;      // pixels
-    uint32_t *gather = nullptr;         // first device: N x frames x shard pixels
-    size_t gather_cap = 0;
-    uint32_t *staging = nullptr;        // first device: frames for a host destination
-    size_t staging_cap = 0;
+    std::vector<ncclComm_t> comm;              // empty with NR_GROUP_COPY
+    std::vector<hipStream_t> cs;               // per rank: its communication stream (on its device)
+    std::vector<uint32_t *> shard[2];          // per set, per rank, on its device: its shards of a call
+    std::vector<size_t> shard_cap[2];          // pixels
+    std::vector<hipEvent_t> sent[2];           // per set, per rank: the set's shards have been read
+    uint32_t *gather[2] = {nullptr, nullptr};  // first device: N x frames x shard pixels
+    size_t gather_cap[2] = {0, 0};
+    uint32_t *staging[2] = {nullptr, nullptr}; // first device: frames for a host destination
+    size_t staging_cap[2] = {0, 0};
+    unsigned long long calls = 0;
 };
 
 namespace {
@@ -50,54 +64,110 @@ int ensure(int device, uint32_t *&p, size_t &cap, size_t pixels) {
     return NR_OK;
 }
 
+void release(nr_group *g) {
+    for (int r = 0; r < (int)g->dev.size(); ++r) {
+        (void)hipSetDevice(g->dev[r]);
+        if (r < (int)g->cs.size() && g->cs[r]) (void)hipStreamSynchronize(g->cs[r]);
+        for (int b = 0; b < 2; ++b) {
+            if (r < (int)g->shard[b].size() && g->shard[b][r]) (void)hipFree(g->shard[b][r]);
+            if (r < (int)g->sent[b].size() && g->sent[b][r]) (void)hipEventDestroy(g->sent[b][r]);
+        }
+        if (r < (int)g->cs.size() && g->cs[r]) (void)hipStreamDestroy(g->cs[r]);
+        if (r < (int)g->comm.size() && g->comm[r]) ncclCommDestroy(g->comm[r]);
+    }
+    if (!g->dev.empty()) {
+        (void)hipSetDevice(g->dev[0]);
+        for (int b = 0; b < 2; ++b) {
+            if (g->gather[b]) (void)hipFree(g->gather[b]);
+            if (g->staging[b]) (void)hipFree(g->staging[b]);
+        }
+    }
+    delete g;
+}
+
 }  // namespace
 
 extern "C" {
 
-int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out) {
-    if (!ctxs || n < 1 || !out) return nr::report_error(NR_E_INVALID, "nr_group_create: bad arguments");
+int nr_group_create_ex(nr_ctx *const *ctxs, int n, int flags, nr_group **out) {
+    if (!ctxs || n < 1 || !out || (flags & ~(NR_GROUP_COPY | NR_GROUP_ASYNC)))
+        return nr::report_error(NR_E_INVALID, "nr_group_create: bad arguments");
     nr_group *g = new nr_group();
     g->n = n;
+    g->flags = flags;
     for (int r = 0; r < n; ++r) {
         if (!ctxs[r]) {
-            delete g;
+            release(g);
             return nr::report_error(NR_E_INVALID, "nr_group_create: context %d is NULL", r);
         }
+        for (int q = 0; q < r; ++q)
+            if (ctxs[q] == ctxs[r]) {
+                release(g);
+                return nr::report_error(NR_E_INVALID, "nr_group_create: context %d appears twice", r);
+            }
         const int d = nr::ctx_device(ctxs[r]);
-        if (std::find(g->dev.begin(), g->dev.end(), d) != g->dev.end()) {
-            delete g;
-            return nr::report_error(NR_E_INVALID, "nr_group_create: two contexts on device %d (one GPU per rank)", d);
+        if (!(flags & NR_GROUP_COPY) && std::find(g->dev.begin(), g->dev.end(), d) != g->dev.end()) {
+            release(g);
+            return nr::report_error(NR_E_INVALID, "nr_group_create: two contexts on device %d (one GPU per rank "
+                                                  "for RCCL; NR_GROUP_COPY shares a GPU)", d);
         }
         g->ctx.push_back(ctxs[r]);
         g->dev.push_back(d);
     }
-    g->comm.resize(n);
-    const ncclResult_t rc = ncclCommInitAll(g->comm.data(), n, g->dev.data());
-    if (rc != ncclSuccess) {
-        delete g;
-        return nr::report_error(NR_E_HIP, "nr_group_create: ncclCommInitAll: %s", ncclGetErrorString(rc));
+    g->cs.assign(n, nullptr);
+    for (int b = 0; b < 2; ++b) {
+        g->shard[b].assign(n, nullptr);
+        g->shard_cap[b].assign(n, 0);
+        g->sent[b].assign(n, nullptr);
     }
-    g->shard.assign(n, nullptr);
-    g->shard_cap.assign(n, 0);
+    for (int r = 0; r < n; ++r) {
+        if (hipSetDevice(g->dev[r]) != hipSuccess || hipStreamCreateWithFlags(&g->cs[r], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g->sent[0][r], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->sent[1][r], hipEventDisableTiming) != hipSuccess) {
+            release(g);
+            return nr::report_error(NR_E_HIP, "nr_group_create: streams / events on device %d", g->dev[r]);
+        }
+    }
+    if (!(flags & NR_GROUP_COPY)) {
+        g->comm.assign(n, nullptr);
+        const ncclResult_t rc = ncclCommInitAll(g->comm.data(), n, g->dev.data());
+        if (rc != ncclSuccess) {
+            g->comm.clear();
+            release(g);
+            return nr::report_error(NR_E_HIP, "nr_group_create: ncclCommInitAll: %s", ncclGetErrorString(rc));
+        }
+    }
     *out = g;
     return NR_OK;
 }
 
+int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out) { return nr_group_create_ex(ctxs, n, 0, out); }
+
 int nr_group_destroy(nr_group *g) {
-    if (!g) return NR_OK;
-    for (int r = 0; r < g->n; ++r) {
-        (void)hipSetDevice(g->dev[r]);
-        if (g->shard[r]) (void)hipFree(g->shard[r]);
-        if (g->comm[r]) ncclCommDestroy(g->comm[r]);
-    }
-    (void)hipSetDevice(g->dev[0]);
-    if (g->gather) (void)hipFree(g->gather);
-    if (g->staging) (void)hipFree(g->staging);
-    delete g;
+    if (g) release(g);
     return NR_OK;
 }
 
 int nr_group_size(const nr_group *g) { return g ? g->n : 0; }
+
+int nr_group_synchronize(nr_group *g) {
+    if (!g) return nr::report_error(NR_E_INVALID, "nr_group_synchronize: NULL group");
+    for (int r = 0; r < g->n; ++r)
+        if (hipSetDevice(g->dev[r]) != hipSuccess || hipStreamSynchronize(g->cs[r]) != hipSuccess)
+            return nr::report_error(NR_E_HIP, "nr_group_synchronize: device %d", g->dev[r]);
+    return NR_OK;
+}
+
+// The gather layout: every rank's set holds frame i's shard at i * shard_px, shard_px = the rows
+// of shard 0 (the most) x W; the gather buffer holds rank r's set at r * per_rank, per_rank =
+// shard_px x nframes; frame i is re-interleaved from gather + i * shard_px with stride per_rank.
+int nr_group_layout(int W, int H, int band, int n, int nframes, size_t *shard_px, size_t *per_rank) {
+    if (W < 1 || H < 1 || band < 1 || n < 1 || nframes < 1 || !shard_px || !per_rank)
+        return nr::report_error(NR_E_INVALID, "nr_group_layout: bad arguments");
+    *shard_px = (size_t)nr_shard_rows(H, band, n, 0) * (size_t)W;
+    *per_rank = *shard_px * (size_t)nframes;
+    return NR_OK;
+}
 
 int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int W, int H, int band, int max_steps,
                           int loc, nr_stats *stats) {
@@ -106,15 +176,21 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
     for (int i = 0; i < nframes; ++i)
         if (!frames[i].out) return nr::report_error(NR_E_INVALID, "nr_group_render_batch: frame %d has no output", i);
     const int n = g->n;
-    const int max_rows = nr_shard_rows(H, band, n, 0);  // shard 0 holds the most rows
-    const size_t shard_px = (size_t)max_rows * W, per_rank = shard_px * (size_t)nframes;
+    size_t shard_px = 0, per_rank = 0;
+    nr_group_layout(W, H, band, n, nframes, &shard_px, &per_rank);
+    const int b = (int)(g->calls & 1);  // this call's buffer set
+    // a set's buffers are reallocated only once the transfers that read them have finished
+    bool grow = per_rank * n > g->gather_cap[b] || (loc != NR_DEVICE && (size_t)W * H * nframes > g->staging_cap[b]);
+    for (int r = 0; r < n; ++r) grow = grow || per_rank > g->shard_cap[b][r];
+    if (grow && nr_group_synchronize(g) != NR_OK) return NR_E_HIP;
     for (int r = 0; r < n; ++r)
-        if (ensure(g->dev[r], g->shard[r], g->shard_cap[r], per_rank) != NR_OK)
+        if (ensure(g->dev[r], g->shard[b][r], g->shard_cap[b][r], per_rank) != NR_OK)
             return nr::report_error(NR_E_HIP, "nr_group_render_batch: shard buffer on device %d", g->dev[r]);
-    if (ensure(g->dev[0], g->gather, g->gather_cap, per_rank * n) != NR_OK ||
-        (loc != NR_DEVICE && ensure(g->dev[0], g->staging, g->staging_cap, (size_t)W * H * nframes) != NR_OK))
+    if (ensure(g->dev[0], g->gather[b], g->gather_cap[b], per_rank * n) != NR_OK ||
+        (loc != NR_DEVICE && ensure(g->dev[0], g->staging[b], g->staging_cap[b], (size_t)W * H * nframes) != NR_OK))
         return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "gather buffer");
-    // ---- every context renders its shard of every frame, in parallel
+    // ---- every context renders its shard of every frame, in parallel, into set b once the
+    // transfer that last read set b is done
     std::vector<int> rc(n, NR_OK);
     std::vector<nr_stats> st(n);
     std::vector<std::string> msg(n);
@@ -124,8 +200,13 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             msg[r] = "hipSetDevice failed";
             return;
         }
+        if (g->calls >= 2 && hipStreamWaitEvent((hipStream_t)nr::ctx_stream(g->ctx[r]), g->sent[b][r], 0) != hipSuccess) {
+            rc[r] = NR_E_HIP;
+            msg[r] = "hipStreamWaitEvent failed";
+            return;
+        }
         std::vector<nr_frame> fr(frames, frames + nframes);
-        for (int i = 0; i < nframes; ++i) fr[i].out = g->shard[r] + (size_t)i * shard_px;
+        for (int i = 0; i < nframes; ++i) fr[i].out = g->shard[b][r] + (size_t)i * shard_px;
         rc[r] = nr_render_batch(g->ctx[r], fr.data(), nframes, W, H, band, n, r, max_steps, NR_DEVICE, &st[r]);
         if (rc[r] == NR_OK) rc[r] = nr_synchronize(g->ctx[r]);  // a fault surfaces here, before the gather
         if (rc[r] != NR_OK) msg[r] = nr_last_error(g->ctx[r]);
@@ -143,34 +224,50 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             const std::string m = "shard " + std::to_string(r) + " (device " + std::to_string(g->dev[r]) + "): " + msg[r];
             return nr::report_error(rc[r], "nr_group_render_batch: %s", m.c_str());
         }
-    // ---- one gather of every frame's shards to the first device
-    ncclResult_t e = ncclGroupStart();
-    for (int r = 0; r < n && e == ncclSuccess; ++r) {
-        e = ncclSend(g->shard[r], per_rank, ncclUint32, 0, g->comm[r], (hipStream_t)nr::ctx_stream(g->ctx[r]));
+    ++g->calls;
+    hipStream_t c0 = g->cs[0];
+    // ---- one gather of every frame's shards to the first device, on the communication streams
+    if (g->flags & NR_GROUP_COPY) {
+        if (hipSetDevice(g->dev[0]) != hipSuccess)
+            return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "hipSetDevice");
+        for (int r = 0; r < n; ++r)
+            if (hipMemcpyPeerAsync(g->gather[b] + (size_t)r * per_rank, g->dev[0], g->shard[b][r], g->dev[r], per_rank * 4,
+                                   c0) != hipSuccess)
+                return nr::report_error(NR_E_HIP, "nr_group_render_batch: shard copy from device %d", g->dev[r]);
+        for (int r = 0; r < n; ++r)
+            if (hipEventRecord(g->sent[b][r], c0) != hipSuccess)
+                return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "event");
+    } else {
+        ncclResult_t e = ncclGroupStart();
+        for (int r = 0; r < n && e == ncclSuccess; ++r)
+            e = ncclSend(g->shard[b][r], per_rank, ncclUint32, 0, g->comm[r], g->cs[r]);
+        for (int r = 0; r < n && e == ncclSuccess; ++r)
+            e = ncclRecv(g->gather[b] + (size_t)r * per_rank, per_rank, ncclUint32, r, g->comm[0], c0);
+        const ncclResult_t e2 = ncclGroupEnd();
+        if (e != ncclSuccess || e2 != ncclSuccess)
+            return nr::report_error(NR_E_HIP, "nr_group_render_batch: RCCL gather: %s",
+                                    ncclGetErrorString(e != ncclSuccess ? e : e2));
+        for (int r = 0; r < n; ++r)
+            if (hipSetDevice(g->dev[r]) != hipSuccess || hipEventRecord(g->sent[b][r], g->cs[r]) != hipSuccess)
+                return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "event");
     }
-    for (int r = 0; r < n && e == ncclSuccess; ++r)
-        e = ncclRecv(g->gather + (size_t)r * per_rank, per_rank, ncclUint32, r, g->comm[0],
-                     (hipStream_t)nr::ctx_stream(g->ctx[0]));
-    const ncclResult_t e2 = ncclGroupEnd();
-    if (e != ncclSuccess || e2 != ncclSuccess)
-        return nr::report_error(NR_E_HIP, "nr_group_render_batch: RCCL gather: %s",
-                                ncclGetErrorString(e != ncclSuccess ? e : e2));
     // ---- re-interleave on the first device: frame i's shard s sits at gather + s * per_rank + i * shard_px
+    if (hipSetDevice(g->dev[0]) != hipSuccess) return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "hipSetDevice");
     for (int i = 0; i < nframes; ++i) {
-        uint32_t *dst = loc == NR_DEVICE ? frames[i].out : g->staging + (size_t)i * W * H;
-        const int a = nr_assemble_shards(g->ctx[0], g->gather + (size_t)i * shard_px, per_rank, dst, W, H, band, n,
-                                         NR_DEVICE);
-        if (a != NR_OK) return a;
+        uint32_t *dst = loc == NR_DEVICE ? frames[i].out : g->staging[b] + (size_t)i * W * H;
+        if (nr::launch_assemble(g->gather[b] + (size_t)i * shard_px, per_rank, dst, W, H, band, n, c0) != hipSuccess)
+            return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "re-interleave launch");
     }
     if (loc != NR_DEVICE) {
-        hipStream_t s0 = (hipStream_t)nr::ctx_stream(g->ctx[0]);
         for (int i = 0; i < nframes; ++i)
-            if (hipMemcpyAsync(frames[i].out, g->staging + (size_t)i * W * H, (size_t)W * H * 4, hipMemcpyDeviceToHost, s0) !=
+            if (hipMemcpyAsync(frames[i].out, g->staging[b] + (size_t)i * W * H, (size_t)W * H * 4, hipMemcpyDeviceToHost, c0) !=
                 hipSuccess)
                 return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "copy to host");
     }
-    const int s = nr_synchronize(g->ctx[0]);
-    if (s != NR_OK) return s;
+    if (!(g->flags & NR_GROUP_ASYNC)) {
+        const int s = nr_group_synchronize(g);
+        if (s != NR_OK) return s;
+    }
     if (stats) {
         nr_stats t{};
         for (int r = 0; r < n; ++r) {

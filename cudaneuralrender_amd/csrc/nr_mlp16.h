@@ -885,6 +885,9 @@ __device__ __noinline__ float mlp16_fp32_call(const float *s, int in0, int nh, f
 // bf16/fp16 tracers' normals (M.x3n): per point, the fp32x3 split for inputs within the x3 pack's
 // bounds, the fp32 MLP otherwise -- the same per-point rule as the fp32x3 precision (mlp16_x3), so
 // a normal never depends on the other rays of its wave.  Oracle: nr_oracle.c mlp_point_gpu_x3.
+// ONE: 64 points as two one-tile passes (the shading site's register budget); otherwise one
+// two-tile pass.
+template <bool ONE = true>
 __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *s32, const uint16_t *lp,
                                                  const float *fl, float fr, float x, float y, float z, uint32_t tmask) {
     const bool in = __builtin_fabsf(x) <= X3_INPUT_BOUND && __builtin_fabsf(y) <= X3_INPUT_BOUND &&
@@ -894,7 +897,7 @@ __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *
         v = mlp16_fp32_call(s32, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
     if (__ballot(in) != 0) {
         float v3;
-        if (tmask & 0xcu) {
+        if (ONE && (tmask & 0xcu)) {
             // two one-tile passes instead of one two-tile pass (fewer live registers at the
             // shading site: 28 -> 9 spilled VGPRs in the bf16 batch tracer, C3 -1.7 %,
             // profiles/r4_ab_x3_tiles.txt): the second on tile 1's points moved to lanes 0-31
@@ -908,7 +911,7 @@ __device__ __forceinline__ float mlp16_x3_normal(const MlpArgs &M, const float *
             const float v1 = mlp16_x3_split(M, lp, fl, lo ? d1 : d0, lo ? a1 : a0, lo ? b1 : b0, lo ? c1 : c0, 0x3u);
             v3 = lo ? v3 : v1;
         } else {
-            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, 0x3u);
+            v3 = mlp16_x3_split(M, lp, fl, fr, x, y, z, tmask);
         }
         v = in ? v3 : v;
     }

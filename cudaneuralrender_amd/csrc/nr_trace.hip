@@ -90,6 +90,18 @@ constexpr int NR_REFILL_MIN_FP32 = 4;
 
 typedef __attribute__((address_space(1))) uint32_t *gptr_u32;
 
+// Phase markers for tools/phase_isa.py (a -DNR_PHASE_MARKS=1 assembly listing only): an assembler
+// comment at each phase boundary of k_trace's loop, so the listing can be cut into refill /
+// shading / fine / compaction / MLP / scene / step and the instructions of each counted.
+#ifndef NR_PHASE_MARKS
+#define NR_PHASE_MARKS 0
+#endif
+#if NR_PHASE_MARKS
+#define NR_PHASE(name) asm volatile("; NRPHASE " #name)
+#else
+#define NR_PHASE(name) ((void)0)
+#endif
+
 constexpr int STASH = 80;  // converged rays waiting for colour, per wave (<= 15 + 64)
 // the A/B knobs' bounds: a shading pass leaves at most SHR - 1 stashed rays, and one
 // iteration adds at most 64; the generated-ray ring is indexed with & (RB - 1)
@@ -298,6 +310,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         rb_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_n);
         rb_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_head);
         if constexpr (EG) nfq = __builtin_amdgcn_readfirstlane(nfq);
+        NR_PHASE(refill);
         // ---- refill free slots from the pixel queue
         if ((!qempty || (DENSE && rb_n > 0)) && !(hold && !T.hold_refill)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
@@ -545,6 +558,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         }
         // the queue drained and no ray left to deal: the tail of the launch
         const bool drained = qempty && (!DENSE || rb_n == 0);
+        NR_PHASE(shading);
         // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass.
         // Once the queue is drained a partial pass waits until the wave's last ray has
         // ended: a pass costs a full MLP latency on the tail's critical path whatever
@@ -594,6 +608,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             nconv += (uint32_t)nb;
             nstash -= nb;
         }
+        NR_PHASE(fine);
         // ---- EG: a fine pass over up to 64 rays of the fine queue (two 32-point tiles) whenever
         // it holds a full tile -- repeated while it does -- and, once the pixel queue is drained,
         // one per iteration (all of them when no coarse ray is left).  The stash holds fewer than
@@ -616,8 +631,9 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
                 // the fp32x3 pack's address made opaque, as in the shading pass
                 int zx = 0;
                 asm volatile("" : "+s"(zx));
-                const float fsdf = mlp16_x3_normal(M, S.s32, M.x3lp + zx, M.x3fl + zx, fr_of(ff), fp.x, fp.y, fp.z,
-                                                   nb > 32 ? 0xfu : 0x3u);
+                // (one two-tile pass: C3 batch 1.85 -> 1.72 ms against two one-tile passes)
+                const float fsdf = mlp16_x3_normal<false>(M, S.s32, M.x3lp + zx, M.x3fl + zx, fr_of(ff), fp.x, fp.y, fp.z,
+                                                          nb > 32 ? 0xfu : 0x3u);
                 nfine += (uint32_t)nb;
                 nsteps += (uint32_t)nb;
                 bool fconv = false, keep = false;
@@ -682,6 +698,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             continue;
         }
         uint32_t tmask = tiles_of(lm);
+        NR_PHASE(compaction);
         // ---- tail / age hold: pack the live rays into the lowest tiles
         if (drained || (hold && !T.hold_refill)) {
             const int nl = (int)__popcll(lm);
@@ -704,10 +721,12 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
                 tmask = (1u << need) - 1u;
             }
         }
+        NR_PHASE(mlp);
         // ---- MLP on every live point, then one sphere-trace step per ray
         if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
         if (MLP_PRIO && !hold) set_priority(MLP_PRIO);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
+        NR_PHASE(step);
         if constexpr (timing) pt[3] += (drained && __popcll(lm) <= 4) ? 1 : 0;
         if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
         if (MLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
@@ -745,7 +764,9 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             }
         }
         if (it >= 0) {
+            NR_PHASE(scene);
             const float ts = scene_sdf(p, sdf, A.scene, zoff_of(rf));
+            NR_PHASE(step);
             if constexpr (timing) {
                 __builtin_amdgcn_s_waitcnt(0);
                 const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -794,6 +815,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         }
         nstash += (int)__popcll(cm);
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
+        NR_PHASE(loop_end);
         const bool h = __ballot(it >= 0 && it >= T.hold_age) != 0;
         if (h != hold) {
             hold = h;

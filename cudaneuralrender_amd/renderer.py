@@ -9,8 +9,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_HOST, NR_PRECISION, NR_SCENE, NR_SCHEDULE,
-                   NRFrame, NRKernelProf, NRStats, check, lib)
+from ._lib import (NR_COLOR_FACING, NR_COLOR_MATCAP, NR_DEVICE, NR_GROUP_ASYNC, NR_GROUP_COPY, NR_HOST, NR_PRECISION,
+                   NR_SCENE, NR_SCHEDULE, NRFrame, NRKernelProf, NRStats, check, lib)
 
 _FP = ctypes.POINTER(ctypes.c_float)
 
@@ -103,6 +103,13 @@ def pack_x3(dims, kernels, biases):
 
 def shard_rows(H, band, nshards, shard):
     return lib().nr_shard_rows(H, band, nshards, shard)
+
+
+def group_layout(W, H, band, n, nframes):
+    """nr_group_layout: (shard_px, per_rank) of nr_group_render_batch's gather buffer."""
+    a, b = ctypes.c_size_t(), ctypes.c_size_t()
+    check(lib().nr_group_layout(W, H, band, n, nframes, ctypes.byref(a), ctypes.byref(b)))
+    return a.value, b.value
 
 
 def batch_frames_per_launch(W, H, band, nshards, shard, nframes, queue_shards=8):
@@ -388,12 +395,19 @@ class Group:
     every shard's status, gathers the shards to the first renderer's GPU in one RCCL call and
     re-interleaves them there (include/neural_render.h nr_group_render_batch)."""
 
-    def __init__(self, renderers):
+    def __init__(self, renderers, copy=False, asynchronous=False):
+        """copy: NR_GROUP_COPY (hipMemcpyPeerAsync transfers; renderers may share a GPU);
+        asynchronous: NR_GROUP_ASYNC (a call returns with its gather enqueued: synchronize())."""
         self._L = lib()
         self.renderers = list(renderers)
         arr = (ctypes.c_void_p * len(self.renderers))(*[r._ctx.value for r in self.renderers])
         self._g = ctypes.c_void_p()
-        check(self._L.nr_group_create(arr, len(self.renderers), ctypes.byref(self._g)))
+        flags = (NR_GROUP_COPY if copy else 0) | (NR_GROUP_ASYNC if asynchronous else 0)
+        check(self._L.nr_group_create_ex(arr, len(self.renderers), flags, ctypes.byref(self._g)))
+
+    def synchronize(self):
+        check(self._L.nr_group_synchronize(self._g))
+        return self
 
     def close(self):
         if self._g:

@@ -184,10 +184,24 @@ int nr_assemble_shards(nr_ctx *ctx, const uint32_t *src, size_t stride_pixels,
  * identical to nr_render on one GPU.  stats: summed over the shards (ms_total: the slowest). */
 typedef struct nr_group nr_group;
 int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out);
+/* flags (round 5): NR_GROUP_COPY moves the shards with hipMemcpyPeerAsync instead of RCCL (the same
+ * layout and re-interleave; contexts may then share a GPU -- how a one-GPU box runs multi-rank
+ * groups); NR_GROUP_ASYNC returns once the call's gather and re-interleave are enqueued on the
+ * group's communication streams, so the next call's render overlaps this call's transfer (shard
+ * and gather buffers are double-buffered): frames[i].out of a call is complete after
+ * nr_group_synchronize -- or, without the flag, when the call returns. */
+#define NR_GROUP_COPY 1
+#define NR_GROUP_ASYNC 2
+int nr_group_create_ex(nr_ctx *const *ctxs, int n, int flags, nr_group **out);
 int nr_group_destroy(nr_group *group);
 int nr_group_size(const nr_group *group);
 int nr_group_render_batch(nr_group *group, const nr_frame *frames, int nframes, int W, int H, int band,
                           int max_steps, int loc, nr_stats *stats);
+int nr_group_synchronize(nr_group *group);
+/* The gather layout nr_group_render_batch uses: frame i's shard on every rank at i * shard_px
+ * (shard_px = nr_shard_rows(H, band, n, 0) * W, the largest shard), rank r's shards at
+ * r * per_rank of the gather buffer (per_rank = shard_px * nframes). */
+int nr_group_layout(int W, int H, int band, int n, int nframes, size_t *shard_px, size_t *per_rank);
 
 /* Replaces NeuralNetwork::forward(X) (neuralNetwork.cpp:54-63) on a batch:
  * X [n][dims[0]] fp32, Y [n][dims[nlayers]] fp32.  loc = NR_HOST or NR_DEVICE. */

@@ -143,3 +143,31 @@ def test_failed_rank_fails_fast(tmp_path, world, bad):
         want = "own" if r == bad else "RankFailed"
         assert res[r][0] == want, res
         assert float(res[r][-1]) < 60, res
+
+
+@pytest.mark.parametrize("n,band,nframes,H", [(2, 1, 3, 131), (3, 8, 3, 131), (3, 5, 2, 41), (2, 8, 1, 7),
+                                              (8, 1, 4, 1024), (3, 1, 1, 1)])
+def test_group_layout_reassembles(n, band, nframes, H):
+    """nr_group_render_batch's gather layout (nr_group_layout: frame i's shard at i * shard_px of
+    every rank's set, rank r's set at r * per_rank) re-interleaved the way it calls the kernel --
+    nr_assemble_shards from gather + i * shard_px with stride per_rank -- gives every frame back,
+    uneven shards (shard_px from shard 0 while the others hold fewer rows) included."""
+    import cudaneuralrender_amd as nr
+    W = 37
+    rng = np.random.default_rng(n * 100 + band)
+    fulls = rng.integers(1, 2**32, size=(nframes, H, W), dtype=np.uint64).astype(np.uint32)
+    shard_px, per_rank = nr.group_layout(W, H, band, n, nframes)
+    assert shard_px == nr.shard_rows(H, band, n, 0) * W and per_rank == shard_px * nframes
+    assert all(nr.shard_rows(H, band, n, s) * W <= shard_px for s in range(n))
+    gather = np.zeros(n * per_rank, np.uint32)
+    for r in range(n):
+        rows = [y for y in range(H) if (y // band) % n == r]
+        for i in range(nframes):   # rank r's set: frame i's shard rows at i * shard_px
+            o = r * per_rank + i * shard_px
+            gather[o:o + len(rows) * W] = fulls[i][rows].reshape(-1)
+    L = nr.lib()
+    for i in range(nframes):
+        out = np.zeros((H, W), np.uint32)
+        src = gather[i * shard_px:]
+        assert L.nr_assemble_shards(None, src.ctypes.data, per_rank, out.ctypes.data, W, H, band, n, 0) == 0
+        assert np.array_equal(out, fulls[i]), (n, band, i)

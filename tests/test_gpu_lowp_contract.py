@@ -82,8 +82,11 @@ def contract(name, geom, size, steps, prec, rows, chrome, record, tau=0.0):
     # >= 0.98 for every C5 crop)
     x = res["vs_exact_mlp"]
     if tau > 0:
-        qi, qiou, qmean = EXACT_BOUND_EG[name]
-        assert x["identical"] >= qi and x["iou"] >= qiou and max(x["mean_abs"][:3]) <= qmean, res
+        ri, riou, rmean = EXACT_EG_R5[(name, geom)]
+        assert x["iou"] >= EG_IOU_TARGET[name], res
+        assert x["identical"] >= ri - 0.02 and max(x["mean_abs"][:3]) <= 1.25 * rmean, res
+        # and never worse than the pure march's r4 figures
+        assert x["identical"] >= EXACT_R4[(name, geom)][0] and x["iou"] >= EXACT_R4[(name, geom)][1], res
     else:
         qi, qiou, qmean = EXACT_BOUND[prec]
         assert x["identical"] >= qi and x["iou"] >= qiou and max(x["mean_abs"][:3]) <= qmean, res
@@ -99,9 +102,13 @@ def contract(name, geom, size, steps, prec, rows, chrome, record, tau=0.0):
 
 # (identical, IoU, max per-channel mean |delta|) against the exact-MLP frame
 EXACT_BOUND = {"bf16": (0.72, 0.90, 12.0), "fp16": (0.75, 0.78, 3.6)}
-# with the endgame (CPU crops of 16 rows, tools/endgame_explore.py at tau = 0.001: C3 0.772 /
-# 1.0 / 2.57, C4 0.950 / 0.997 / 10.3, C5 0.779-0.996 / 0.998-0.99994 / 1.33-2.40)
-EXACT_BOUND_EG = {"C3": (0.74, 0.99, 4.0), "C4": (0.92, 0.99, 12.0), "C5": (0.74, 0.98, 3.0)}
+# with the endgame at NR_ENDGAME_DEFAULT (round 5, profiles/r5_lowp_contract.json): coverage IoU to
+# VERDICT r4's targets, identical pixels and mean |delta| within 2 points / 1.25x of the measured
+EG_IOU_TARGET = {"C3": 0.99, "C4": 0.99, "C5": 0.98}
+EXACT_EG_R5 = {("C3", "car_1"): (0.7795, 0.99997, 2.082), ("C4", "plane_2"): (0.8921, 0.99935, 4.5724),
+               ("C5", "plane_1"): (0.9017, 0.99892, 2.3629), ("C5", "plane_2"): (0.9324, 0.99991, 2.1207),
+               ("C5", "plane_3"): (0.9961, 0.99865, 0.982), ("C5", "car_1"): (0.7726, 0.99993, 1.9887),
+               ("C5", "3a3d4a90a2db90b4203936772104a82d.obj"): (0.8832, 0.99934, 2.1852)}
 EXACT_R4 = {("C3", "car_1"): (0.7398, 0.99801, 5.629), ("C4", "plane_2"): (0.8367, 0.93107, 10.447),
             ("C5", "plane_1"): (0.8543, 0.86754, 3.266), ("C5", "plane_2"): (0.9205, 0.97787, 2.978),
             ("C5", "plane_3"): (0.9922, 0.81736, 1.412), ("C5", "car_1"): (0.7634, 0.99674, 2.687),

@@ -40,7 +40,7 @@ def test_renderer_single_png(tmp_path, matcap, scene):
     assert "volumeRender, Throughput =" in p.stdout
     png = nr.load_png(str(tmp_path / "plane_1.h5.png"))
     dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
-    iv, nm = nr.camera(-20, 30, 2.0, mode="eigen")  # the CLI's default camera arithmetic
+    iv, nm = nr.camera(-20, 30, 2.0)  # the CLI's default camera arithmetic (f64, rounded once)
     mc = nr.load_png(nr.matcap_path(matcap)) if matcap else None
     ref, _ = oracle.OracleNet(K, B).render(96, 80, iv, nm, color_type=1 if matcap else 0,
                                            scene=0 if scene == "v1" else 1, matcap=mc, max_steps=128)
@@ -63,22 +63,23 @@ def test_renderer_spin(tmp_path):
     mc = nr.load_png(nr.matcap_path("Chrome"))
     net = oracle.OracleNet(K, B)
     for i in (0, 45, 200, 359):
-        iv, nm = nr.camera(-15, float(i), 2.0, mode="eigen")
+        iv, nm = nr.camera(-15, float(i), 2.0)
         ref, _ = net.render(24, 20, iv, nm, frame=i, color_type=1, matcap=mc, max_steps=96)
         png = nr.load_png(str(tmp_path / f"{i:03d}.png"))
         assert np.array_equal(png, ref[::-1, ::-1]), i
 
 
-def test_renderer_camera_f64(tmp_path):
-    """--camera f64: the frame of nr_camera's f64 matrices (the library's default camera)."""
+def test_renderer_camera_eigen(tmp_path):
+    """--camera eigen: the frame of nr_camera_ex's restatement of Eigen's scalar float path
+    (unpinned against the reference's SSE build; the CLI default is f64)."""
     args = [os.path.join(BIN, "neuralSDFRenderer"), "-i", nr.geometry_path("plane_1"), "-o", str(tmp_path) + "/",
             "-W", "64", "-H", "48", "-rx", "-33.3", "-ry", "71.7", "--single", "--max-steps", "128",
-            "-M", nr.matcap_path("Chrome"), "--camera", "f64"]
+            "-M", nr.matcap_path("Chrome"), "--camera", "eigen"]
     p = run(args)
     assert p.returncode == 0, p.stdout + p.stderr
     png = nr.load_png(str(tmp_path / "plane_1.h5.png"))
     dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
-    iv, nm = nr.camera(-33.3, 71.7, 2.0)
+    iv, nm = nr.camera(-33.3, 71.7, 2.0, mode="eigen")
     ref, _ = oracle.OracleNet(K, B).render(64, 48, iv, nm, color_type=1, matcap=nr.load_png(nr.matcap_path("Chrome")),
                                            max_steps=128)
     assert np.array_equal(png, ref[::-1, ::-1])

@@ -32,11 +32,13 @@ ap.add_argument("--batch", type=int, default=8, help="frames per nr_render_batch
 ap.add_argument("--only", default="", help="comma-separated config names to run (default all)")
 ap.add_argument("--bpc", type=int, default=0, help="nr_set_occupancy (0: the library's default)")
 ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (A/B of the bf16 ReLU forms: 512)")
+ap.add_argument("--endgame", default="", help="comma-separated nr_set_endgame thresholds to run each 16-bit config "
+                "with (default: the library's, NR_ENDGAME_DEFAULT; 0 = the pure 16-bit march)")
 a = ap.parse_args()
 matcap = nr.load_png(nr.matcap_path("Chrome"))
 
 
-def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1):
+def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1, tau=None):
     evals = (st["ray_steps"] + st["shade_evals"]) / nframes
     rs = st["ray_steps"] / nframes
     res = {"config": name, "geometry": geom, "size": size, "precision": prec, "max_steps": steps,
@@ -44,13 +46,25 @@ def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1):
            "Mray_steps_per_s": round(rs / t / 1e3, 1),
            "TFLOPs": round(evals * FLOP / t / 1e9, 2),
            "frac_of_peak": round(evals * FLOP / t / 1e9 / PEAK[prec], 4)}
+    if prec != "fp32":
+        res["endgame_tau"] = tau
+        res["fp32x3_share"] = round(st.get("endgame_evals", 0) / max(st["ray_steps"], 1), 4)
     print(json.dumps(res), flush=True)
 
 
 def run(name, geom, size, prec, steps, shard=None):
     if a.only and name not in a.only.split(","):
         return
+    taus = [float(t) for t in a.endgame.split(",")] if a.endgame and prec != "fp32" else [None]
+    for tau in taus:
+        run1(name, geom, size, prec, steps, shard, tau)
+
+
+def run1(name, geom, size, prec, steps, shard, tau):
     r = nr.Renderer(0).load_h5(nr.geometry_path(geom)).set_precision(prec)
+    if tau is not None:
+        r.set_endgame(tau)
+    tau = nr.NR_ENDGAME_DEFAULT if tau is None else tau
     r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
     r.set_debug(a.debug)
     r.set_occupancy(a.bpc)
@@ -62,7 +76,7 @@ def run(name, geom, size, prec, steps, shard=None):
         st = r.render_shard_device(out[0].data_ptr(), size, size, band, nsh, shard or 0, steps, with_stats=True)
         if i >= 2:
             ms.append(st["ms_total"])
-    report(name, geom, size, prec, steps, shard, "single", float(np.median(ms)), st)
+    report(name, geom, size, prec, steps, shard, "single", float(np.median(ms)), st, tau=tau)
     if a.batch > 0:
         iv, nm = nr.camera(0.0, 0.0, 2.0)
         cams = [(iv, nm, 0)] * a.batch
@@ -72,7 +86,7 @@ def run(name, geom, size, prec, steps, shard=None):
             st = r.render_batch_device(ptrs, size, size, cams, steps, band, nsh, shard or 0, with_stats=True)
             if i >= 1:
                 ms.append(st["ms_total"])
-        report(name, geom, size, prec, steps, shard, f"batch{a.batch}", float(np.median(ms)) / a.batch, st, a.batch)
+        report(name, geom, size, prec, steps, shard, f"batch{a.batch}", float(np.median(ms)) / a.batch, st, a.batch, tau)
     r.close()
 
 
