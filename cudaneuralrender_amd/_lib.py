@@ -28,7 +28,7 @@ EXPORTS = [
     "nr_assemble_shards", "nr_mlp_forward", "nr_layer_forward", "nr_camera", "nr_camera_ex", "nr_h5_read_keras",
     "nr_png_load", "nr_png_save", "nr_ppm_save", "nr_free", "nr_set_profiling", "nr_prof_collect",
     "nr_set_poll_interval", "nr_set_schedule", "nr_set_debug", "nr_debug_stamps",
-    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_age_hold", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
+    "nr_set_occupancy", "nr_set_temporal_order", "nr_dense_forward", "nr_set_pixel_spread", "nr_set_cost_probe", "nr_set_wave_rays", "nr_set_queue_shards", "nr_set_layer_chunk", "nr_batch_frames_per_launch",
     "nr_h5_open", "nr_h5_close", "nr_h5_root", "nr_h5_object_type", "nr_h5_num_members", "nr_h5_member",
     "nr_h5_dims", "nr_h5_read_f32",
     "nr_group_create", "nr_group_destroy", "nr_group_size", "nr_group_render_batch", "nr_pack_x3",
@@ -152,7 +152,6 @@ def lib():
         "nr_set_debug": (I, [P, I]),
         "nr_set_endgame": (I, [P, F]),
         "nr_set_occupancy": (I, [P, I]),
-        "nr_set_age_hold": (I, [P, I, I]),
         "nr_set_pixel_spread": (I, [P, I]),
         "nr_set_cost_probe": (I, [P, I, I]),
         "nr_set_wave_rays": (I, [P, I]),

@@ -59,8 +59,6 @@ struct nr_ctx {
     int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
     // temporal block ordering (nr_set_temporal_order)
     int temporal = 0;
-    // age hold (nr_set_age_hold)
-    int hold_age = 0, hold_prio = 2;
     int spread = -1;  // nr_set_pixel_spread; -1 = auto (spread_for)
     int probe_steps = 0, probe_take = 16, probe_dilate = 1;  // nr_set_cost_probe
     int wave_rays = 0;  // nr_set_wave_rays (0: automatic, wave_rays_for)
@@ -937,9 +935,6 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     T.nq_shift = c->nq_shift;
     T.bw = (W + 7) / 8;
     T.nblocks = T.bw * ((rows + 7) / 8);
-    T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
-    T.hold_prio = c->hold_prio & 3;
-    T.hold_refill = c->hold_prio >= 4;
     {
         const int sp = spread_for(c, nframes, npix);
         T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;
@@ -1096,9 +1091,6 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         const int bw = (W + 7) / 8, bh = (rows + 7) / 8;
         T.bw = bw;
         T.nblocks = bw * bh;
-        T.hold_age = c->hold_age > 0 ? c->hold_age : INT_MAX;
-        T.hold_prio = c->hold_prio & 3;
-        T.hold_refill = c->hold_prio >= 4;
         T.itmap = (c->debug & 8) != 0;
         T.eg_tau = endgame_tau(c, max_steps);
         {
@@ -1141,7 +1133,6 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             P.order = nullptr;
             P.bcost = c->d_bcost;
             P.spread_shift = 0;
-            P.hold_age = INT_MAX;
             RenderArgs Ap = A;
             Ap.max_steps = std::min(max_steps, c->probe_steps);
             const long pwaves = ((long)T.nblocks + P.take - 1) / P.take;
@@ -1370,13 +1361,6 @@ int nr_set_temporal_order(nr_ctx *c, int on) {
     if (!c) return set_err(nullptr, NR_E_INVALID, "ctx is NULL");
     c->temporal = on < 0 ? 0 : (on > 2 ? 2 : on);
     c->order_valid = 0;
-    return NR_OK;
-}
-
-int nr_set_age_hold(nr_ctx *c, int age, int prio) {
-    if (!c || age < 0 || prio < 0 || prio > 7) return set_err(c, NR_E_INVALID, "nr_set_age_hold: bad arguments");
-    c->hold_age = age;
-    c->hold_prio = prio;
     return NR_OK;
 }
 

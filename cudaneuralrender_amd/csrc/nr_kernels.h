@@ -100,9 +100,6 @@ struct TraceArgs {
     const uint32_t *order;
     uint32_t *bcost;
     int bw, nblocks;            // blocks per row, blocks in the shard image
-    // age hold: a wave holding a ray of >= hold_age iterations stops refilling, packs
-    // its rays into the lowest tiles and issues at priority hold_prio (INT_MAX = off)
-    int hold_age, hold_prio, hold_refill;  // hold_refill: priority only, keep refilling
     // pixel spread: the queue deals a group of 2^spread_shift blocks pixel-major (a refill
     // takes one pixel from each of 64 blocks), so a block of long rays is marched by 64
     // different waves instead of one (0/1 = block-major)

@@ -276,7 +276,6 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
     uint32_t pool_base = 0, pool_cnt = 0, pend_v = 0;  // NR_QUEUE_PREFETCH state
     bool pend = false;
     uint32_t rb_n = 0, rb_head = 0;  // DENSE: rays in the wave's buffer, ring position of the first
-    bool hold = false;  // age hold (TraceArgs::hold_age): no refill, packed tiles, raised priority
     F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
     float tfar = 0.0f;
     uint32_t pix = 0;
@@ -312,7 +311,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         if constexpr (EG) nfq = __builtin_amdgcn_readfirstlane(nfq);
         NR_PHASE(refill);
         // ---- refill free slots from the pixel queue
-        if ((!qempty || (DENSE && rb_n > 0)) && !(hold && !T.hold_refill)) {
+        if (!qempty || (DENSE && rb_n > 0)) {
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
             const uint64_t freem = __ballot(it < 0) & T.lane_cap;
@@ -699,8 +698,8 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         }
         uint32_t tmask = tiles_of(lm);
         NR_PHASE(compaction);
-        // ---- tail / age hold: pack the live rays into the lowest tiles
-        if (drained || (hold && !T.hold_refill)) {
+        // ---- tail: pack the live rays into the lowest tiles
+        if (drained) {
             const int nl = (int)__popcll(lm);
             const int need = (nl + 15) >> 4;
             if (__popc(tmask) > need) {
@@ -723,13 +722,13 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         }
         NR_PHASE(mlp);
         // ---- MLP on every live point, then one sphere-trace step per ray
-        if (NONMLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
-        if (MLP_PRIO && !hold) set_priority(MLP_PRIO);
+        if (NONMLP_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (MLP_PRIO) set_priority(MLP_PRIO);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         NR_PHASE(step);
         if constexpr (timing) pt[3] += (drained && __popcll(lm) <= 4) ? 1 : 0;
-        if (NONMLP_PRIO && !hold) set_priority(NONMLP_PRIO);
-        if (MLP_PRIO && !hold) __builtin_amdgcn_s_setprio(0);
+        if (NONMLP_PRIO) set_priority(NONMLP_PRIO);
+        if (MLP_PRIO) __builtin_amdgcn_s_setprio(0);
         if constexpr (timing) {
             __builtin_amdgcn_s_waitcnt(0);
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -816,11 +815,6 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         nstash += (int)__popcll(cm);
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[4] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         NR_PHASE(loop_end);
-        const bool h = __ballot(it >= 0 && it >= T.hold_age) != 0;
-        if (h != hold) {
-            hold = h;
-            set_priority(h ? T.hold_prio : 0);
-        }
     }
     // ---- frame statistics: one set of atomics per wave
 #pragma unroll

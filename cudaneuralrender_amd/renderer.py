@@ -235,12 +235,6 @@ class Renderer:
         self._chk(self._L.nr_set_occupancy(self._ctx, int(blocks_per_cu)))
         return self
 
-    def set_age_hold(self, age, prio=2):
-        """Persistent schedule: a wave with a ray older than `age` iterations stops
-        refilling, compacts its rays and runs at issue priority `prio` (age 0 = off)."""
-        self._chk(self._L.nr_set_age_hold(self._ctx, int(age), int(prio)))
-        return self
-
     def set_pixel_spread(self, group_blocks):
         """Persistent schedule: deal each group of `group_blocks` 8x8 blocks pixel-major
         (0 = block-major; -1 = automatic, the default: 16 for one-frame launches, 0 for

@@ -288,12 +288,6 @@ int nr_set_queue_shards(nr_ctx *ctx, int n);
  * layer scratch: 2 x points x widest hidden layer x 4 B).  0 = auto (128 MiB per buffer).
  * The reference sizes Z for the whole batch, W*H*4 points (volumeRender_kernel.cu:659-661). */
 int nr_set_layer_chunk(nr_ctx *ctx, long points);
-/* Age hold (persistent schedule): a wave holding a ray that has marched `age` or more
- * iterations stops taking new pixels, packs its live rays into the fewest 16-ray tiles
- * and raises its issue priority to `prio` (0-3) until they finish, so long rays march
- * at a short per-iteration latency while the other waves keep the matrix cores busy
- * (age 0 = off).  Pixels are unaffected. */
-int nr_set_age_hold(nr_ctx *ctx, int age, int prio);
 /* Pixel spread (persistent schedule): the pixel queue deals each group of
  * `group_blocks` 8x8 blocks pixel-major -- one refill takes one pixel from each of up
  * to 64 blocks -- so the rays of one slow block are spread over many waves (0 =

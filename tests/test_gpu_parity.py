@@ -323,16 +323,15 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
         rend.set_pixel_spread(-2)  # -1 is "automatic"
     ref, sref = rend.set_pixel_spread(0).render(W, H, 128)
     try:
-        for spread, age, prio, bpc in [(16, 0, 0, 0), (64, 0, 0, 3), (1024, 0, 0, 1), (1, 0, 0, 0), (16, 32, 2, 3),
-                                       (0, 8, 3, 2), (-1, 0, 0, 0)]:
-            rend.set_pixel_spread(spread).set_age_hold(age, prio).set_occupancy(bpc)
+        for spread, bpc in [(16, 0), (64, 3), (1024, 1), (1, 0), (16, 3), (0, 2), (-1, 0)]:
+            rend.set_pixel_spread(spread).set_occupancy(bpc)
             img, st = rend.render(W, H, 128)
-            assert np.array_equal(img, ref), (spread, age, prio, bpc)
+            assert np.array_equal(img, ref), (spread, bpc)
             for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
-                assert st[k] == sref[k], (k, spread, age, prio, bpc)
+                assert st[k] == sref[k], (k, spread, bpc)
         # rays per wave: explicit 64 / 32 and automatic (0: 32 for an fp32 launch of at most 2x
         # its waves' slots, this frame on 8 shards)
-        rend.set_pixel_spread(-1).set_age_hold(0, 2).set_occupancy(0)
+        rend.set_pixel_spread(-1).set_occupancy(0)
         for rays in (64, 32, 0):
             rend.set_wave_rays(rays)
             img, st = rend.render(W, H, 128)
@@ -346,7 +345,7 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
         with pytest.raises(nr.NRError):
             rend.set_wave_rays(-1)
     finally:
-        rend.set_pixel_spread(-1).set_age_hold(0, 2).set_occupancy(0).set_wave_rays(0)
+        rend.set_pixel_spread(-1).set_occupancy(0).set_wave_rays(0)
 
 
 def test_iteration_map(rend, nets, chrome):

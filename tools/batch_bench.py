@@ -25,7 +25,6 @@ ap.add_argument("--spread", type=int, default=-1, help="nr_set_pixel_spread (blo
 ap.add_argument("--queues", type=int, default=8, help="nr_set_queue_shards")
 ap.add_argument("--temporal", type=int, default=0, help="nr_set_temporal_order")
 ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (1024: frame-major batch queue)")
-ap.add_argument("--hold", type=int, default=0, help="nr_set_age_hold age (0: off)")
 ap.add_argument("--band", type=int, default=1, help="rows per band dealt round-robin (bench.py BAND)")
 ap.add_argument("--single", action="store_true",
                 help="time one-frame launches through nr_render_shard (the one-frame k_trace instance) "
@@ -38,8 +37,6 @@ r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
 r.set_occupancy(a.bpc).set_wave_rays(a.rays).set_schedule(a.schedule)
 r.set_pixel_spread(a.spread).set_queue_shards(a.queues).set_temporal_order(a.temporal)
 r.set_debug(a.debug)
-if a.hold:
-    r.set_age_hold(a.hold)
 S = a.size
 bufs = [torch.zeros(S * S, dtype=torch.int32, device="cuda") for _ in range(32)]
 for n in (int(x) for x in a.shards.split(",")):
@@ -61,4 +58,4 @@ for n in (int(x) for x in a.shards.split(",")):
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
         line.append(f"{'single' if a.single and b == 1 else 'batch'} {b}: {dt:.3f} ms/frame")
-    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} debug {a.debug} band {a.band} hold {a.hold}: " + "  ".join(line), flush=True)
+    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} debug {a.debug} band {a.band}: " + "  ".join(line), flush=True)

@@ -30,7 +30,7 @@ for spec in a.grid.split(";"):
     bpc, age, prio, temporal, spread, pst, ptake = v[:7]
     r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
     r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
-    r.set_occupancy(bpc).set_age_hold(age, prio).set_temporal_order(temporal).set_pixel_spread(spread)
+    r.set_occupancy(bpc).set_temporal_order(temporal).set_pixel_spread(spread)
     r.set_cost_probe(pst, ptake)
     for _ in range(3):
         r.render_device(out.data_ptr(), a.size, a.size, a.steps)

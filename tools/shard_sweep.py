@@ -26,7 +26,7 @@ for spec in a.grid.split(";"):
     bpc, age, prio, spread, rays, nq = v[:6]
     r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
     r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(matcap)
-    r.set_occupancy(bpc).set_age_hold(age, prio).set_pixel_spread(spread).set_wave_rays(rays).set_queue_shards(nq)
+    r.set_occupancy(bpc).set_pixel_spread(spread).set_wave_rays(rays).set_queue_shards(nq)
     line = []
     for n in (1, 2, 4, 8):
         ms = []

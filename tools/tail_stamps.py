@@ -28,7 +28,7 @@ r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precisio
 r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(nr.load_png(nr.matcap_path("Chrome")))
 r.set_occupancy(a.bpc)
 r.set_temporal_order(a.temporal)
-r.set_pixel_spread(a.spread).set_age_hold(a.hold, 2).set_wave_rays(a.rays).set_queue_shards(a.queues)
+r.set_pixel_spread(a.spread).set_wave_rays(a.rays).set_queue_shards(a.queues)
 for _ in range(3):
     r.render_shard(a.size, a.size, 8, a.nshards, 0, a.steps)
 r.set_debug(1)
