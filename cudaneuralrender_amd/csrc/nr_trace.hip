@@ -201,7 +201,9 @@ __device__ __forceinline__ void set_priority(int prio) {
 // outside), the scene and singleMarch's step -- and returns the survivors to the queue.  So the
 // switch iteration's step, the convergence test (:474), the background test and every later step
 // of the ray are decided in fp32x3, on full tiles.  Oracle: nr_oracle.c or_set_endgame.
-// (3 workgroups per CU: the fine queue's 13 KB of LDS leaves room for no more)
+// (3 workgroups per CU: the fine pass's registers -- 161 VGPRs; at 4 per CU, <= 128 VGPRs, the
+// spills cost C3 +25 %, C5 +40-55 %; a pass per 64 queued rays instead of 32: C5 batch +5-10 %;
+// profiles/r5_ab_eg.txt)
 #ifndef NR_TRACE_BPC_EG
 #define NR_TRACE_BPC_EG 3
 #endif

@@ -36,11 +36,13 @@ extern "C" {
 
 /* MLP arithmetic for the 32x32 hidden layers */
 #define NR_PRECISION_FP32 0  /* bit-exact with the CPU oracle (f32 MFMA = fmaf chain) */
-#define NR_PRECISION_BF16 1  /* bf16 MFMA, f32 accumulate; normals evaluated in fp32 */
-#define NR_PRECISION_FP16 2  /* fp16 MFMA, f32 accumulate; normals evaluated in fp32 */
+#define NR_PRECISION_BF16 1  /* bf16 MFMA, f32 accumulate; normals (the 4 tetrahedron samples) in fp32x3,
+                                 nr_set_debug bit 15: fp32; rays near a surface finish in fp32x3
+                                 (nr_set_endgame, on by default) */
+#define NR_PRECISION_FP16 2  /* fp16 MFMA, f32 accumulate; normals and endgame as bf16 */
 #define NR_PRECISION_FP32X3 3 /* fp32-class on the fp16 matrix core: three-term split a.w ~ ah.wh + al.wh + ah.wl,
                                   f32 accumulate (~2-3x the f32 chain's error against an exact
-                                  evaluation); normals evaluated in fp32 (bit-exact); waves with
+                                  evaluation); normals evaluated in fp32 (bit-exact); points with
                                   inputs outside the pack's bounds run the fp32 MLP */
 
 /* scene composition, sceneSDF (volumeRender_kernel.cu:217-230) */

@@ -14,7 +14,7 @@ for lib in ${LIBS:-default}; do
   if [ -n "$TESTS" ]; then
     timeout -k 10 300 python -u -m pytest $TESTS -m gpu -x -q --timeout 120 --timeout-method thread >> $O 2>&1 || exit 1
   fi
-  for n in 16777216 67108864; do
+  for n in ${SIZES:-16777216 67108864}; do
     timeout -k 10 120 python -u tools/mlp_bench.py --n $n --iters 20 --precision ${PRECS:-bf16} --bpc ${BPC:-8} 2>&1 | grep -v amdgpu.ids >> $O || exit 1
   done
 done

@@ -196,8 +196,9 @@ def build(prec, clamp, nt=4):
     return st
 
 
-def check(st):
-    """Verifies every hazard of the stream (raises on the first violation)."""
+def check(st, inputs=None):
+    """Verifies every hazard of the stream (raises on the first violation).  inputs: the registers
+    the compiler's VALU wrote just before the stream (default: the k-step-0 B operands)."""
     L = Layout(getattr(st, "nt", 4))
     pos = []   # wait-state position of each instruction
     p = 0
@@ -205,7 +206,9 @@ def check(st):
         pos.append(p)
         p += ins[4]
     # the input B operands (k-step 0 slots) were written by the compiler's VALU just before the stream
-    last_w = {r: (-1, "valu") for t in range(L.nt) for r in rng(L.KOP(t, 0), 4)}
+    if inputs is None:
+        inputs = [r for t in range(L.nt) for r in rng(L.KOP(t, 0), 4)]
+    last_w = {r: (-1, "valu") for r in inputs}
     last_r = {}      # reg -> list of (index, operand role) of MFMA reads since the last write
     pending = set()  # regs with an LDS load not yet waited for
     for i, (text, kind, reads, writes, _) in enumerate(st.ins):
