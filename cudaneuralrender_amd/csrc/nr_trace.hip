@@ -297,6 +297,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
     constexpr bool timing = STAMPS;
     const long gwave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     unsigned long long t_start = STAMPS ? __builtin_amdgcn_s_memrealtime() : 0ull, t_empty = 0ull;
+    int nl_drain = -1;  // stamps: live rays at the first iteration after the drain
     while (true) {
         if constexpr (timing) tph = __builtin_amdgcn_s_memtime();
         // The loop's control state is wave-uniform (the whole wave is active here);
@@ -728,7 +729,12 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         if (MLP_PRIO) set_priority(MLP_PRIO);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         NR_PHASE(step);
-        if constexpr (timing) pt[3] += (drained && __popcll(lm) <= 4) ? 1 : 0;
+        if constexpr (timing) {
+            // iterations with <= 4 rays (low word) and ray-steps (high word) after the drain; the
+            // live rays when the wave first saw the queue drained
+            pt[3] += drained ? ((__popcll(lm) <= 4 ? 1ull : 0ull) | ((unsigned long long)__popcll(lm) << 32)) : 0ull;
+            if (drained && nl_drain < 0) nl_drain = (int)__popcll(lm);
+        }
         if (NONMLP_PRIO) set_priority(NONMLP_PRIO);
         if (MLP_PRIO) __builtin_amdgcn_s_setprio(0);
         if constexpr (timing) {
@@ -823,7 +829,8 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
     for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
     if (STAMPS && lane == 0) {
         unsigned long long *st = T.stamps + 16 * gwave;
-        st[0] = t_start; st[1] = t_empty; st[2] = __builtin_amdgcn_s_memrealtime();
+        st[0] = t_start; st[1] = t_empty | ((unsigned long long)(nl_drain < 0 ? 0 : nl_drain) << 56);
+        st[2] = __builtin_amdgcn_s_memrealtime();
         st[3] = ((unsigned long long)wit_tail << 32) | wit;
         for (int i = 0; i < 8; ++i) st[4 + i] = ph[i];
         for (int i = 0; i < 4; ++i) st[12 + i] = pt[i];

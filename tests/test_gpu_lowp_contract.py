@@ -125,7 +125,8 @@ def record():
         json.dump(out, f, indent=1)
 
 
-TAUS = [0.0, nr.NR_ENDGAME_DEFAULT]
+# NR_TEST_EG_TAU: another threshold for the endgame cases (exploration; the targets still apply)
+TAUS = [0.0, float(os.environ.get("NR_TEST_EG_TAU", nr.NR_ENDGAME_DEFAULT))]
 TAU_IDS = ["pure", "endgame"]
 
 

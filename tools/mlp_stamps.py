@@ -19,7 +19,7 @@ r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1"))
 r.set_stream(torch.cuda.current_stream().cuda_stream)
 for prec in sys.argv[1].split(",") if len(sys.argv) > 1 else ("bf16", "fp16"):
     r.set_precision(prec)
-    for debug in (0, 4096):
+    for debug in (0,):
         r.set_debug(debug)
         for bpc in (3,):
             r.set_occupancy(bpc)

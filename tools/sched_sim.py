@@ -42,10 +42,13 @@ def spread_order(m, G=16):
     return np.concatenate(out)
 
 
-def simulate(costs, bpc=2, merge_pairs=False, take=64):
-    """costs: iteration counts in dispense order.  Returns (frame_us, drain_us)."""
+def simulate(costs, bpc=2, merge_pairs=False, take=64, share=0):
+    """costs: iteration counts in dispense order.  Returns (frame_us, drain_us).
+    share > 0: once the queue is drained, a wave holding more than `share` rays moves the rest to a
+    global pool and a wave holding fewer takes from it (tail sharing through HBM, ideal)."""
     q = 0
     n = len(costs)
+    pool = []
     waves = [[np.zeros(64, np.int32) for _ in range(bpc)] for _ in range(NSIMD)]
     ev = [(0.0, s) for s in range(NSIMD)]
     heapq.heapify(ev)
@@ -71,6 +74,16 @@ def simulate(costs, bpc=2, merge_pairs=False, take=64):
                 k = min(len(free), n - q, take)
                 w[free[:k]] = costs[q:q + k]
                 q += k
+            if share and q >= n:
+                live = np.flatnonzero(w > 0)
+                if len(live) > share:
+                    pool.extend(w[live[share:]].tolist())
+                    w[live[share:]] = 0
+                elif len(live) < share and pool:
+                    k = min(share - len(live), len(pool))
+                    fr = np.flatnonzero(w == 0)[:k]
+                    w[fr] = pool[-k:]
+                    del pool[-k:]
             nl = int((w > 0).sum())
             if nl == 0:
                 continue
@@ -82,7 +95,7 @@ def simulate(costs, bpc=2, merge_pairs=False, take=64):
             mfma += tiles * T_TILE
             crit = max(crit, tiles * T_TILE + V_WAVE)
         if not any_live:
-            if q >= n:
+            if q >= n and not pool:
                 t_end = max(t_end, t)
                 continue
             heapq.heappush(ev, (t + 0.5, s))
@@ -192,12 +205,14 @@ def main():
         ("temporal bpc3", block_order(m, bmax), 3, False),
         ("spread16 merge", spread_order(m, 16), 2, True),
         ("spread16 bpc3 merge", spread_order(m, 16), 3, True),
+        ("spread16 bpc3 share16", spread_order(m, 16), 3, 16),
+        ("spread16 bpc3 share32", spread_order(m, 16), 3, 32),
     ]
     only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
     for name, costs, bpc, merge in cases:
         if only and name not in only:
             continue
-        t, d = simulate(costs, bpc, merge)
+        t, d = simulate(costs, bpc, merge is True, share=merge if not isinstance(merge, bool) else 0)
         print(f"{name:24s} frame {t / 1e3:.3f} ms  drain {d / 1e3:.3f} ms  tail {(t - d) / 1e3:.3f} ms", flush=True)
     for age, dil in [(16, True), (24, True), (32, True), (24, False)]:
         t, d = simulate_promote(m, age, dil)

@@ -19,10 +19,10 @@ ap.add_argument("--steps", type=int, default=128)
 ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--temporal", type=int, default=0)
 ap.add_argument("--spread", type=int, default=0)
-ap.add_argument("--hold", type=int, default=0)
 ap.add_argument("--nshards", type=int, default=1)
 ap.add_argument("--rays", type=int, default=0)
 ap.add_argument("--queues", type=int, default=8)
+ap.add_argument("--out", default="", help="save the per-wave stamps (npz)")
 a = ap.parse_args()
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
 r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(nr.load_png(nr.matcap_path("Chrome")))
@@ -36,10 +36,12 @@ img, st = r.render_shard(a.size, a.size, 8, a.nshards, 0, a.steps)
 s = r.debug_stamps().astype(np.int64)
 s = s[s[:, 2] > 0]
 t0 = s[:, 0].min()
+nl_drain = s[:, 1] >> 56
+s[:, 1] &= (1 << 56) - 1
 start, empty, end = (s[:, 0] - t0) / 100.0, s[:, 1], (s[:, 2] - t0) / 100.0
 wit, wit_tail = s[:, 3] & 0xffffffff, s[:, 3] >> 32
 empty = np.where(empty > 0, (empty - t0) / 100.0, np.nan)
-print(f"== bpc {a.bpc} temporal {a.temporal} spread {a.spread} hold {a.hold} rays {a.rays} queues {a.queues} "
+print(f"== bpc {a.bpc} temporal {a.temporal} spread {a.spread} rays {a.rays} queues {a.queues} "
       f"nshards {a.nshards} precision {a.precision}: stats {st}")
 print(f"waves {len(s)}  start spread {start.max():.1f} us  kernel span {end.max():.1f} us")
 print(f"queue drained: first {np.nanmin(empty):.1f} us  median {np.nanmedian(empty):.1f} us  last {np.nanmax(empty):.1f} us")
@@ -66,9 +68,16 @@ for i in last[-3:]:
     print(f"  wave ending {end[i]:.1f} us: cycles/iter refill {ph[i,0]/max(wit[i],1):.0f} shading {ph[i,1]/max(wit[i],1):.0f} "
           f"mlp {ph[i,2]/max(wit[i],1):.0f} scene {ph[i,3]/max(wit[i],1):.0f} step {ph[i,4]/max(wit[i],1):.0f}")
 tl = s[:, 12:15].astype(np.float64)
+tail_steps = s[:, 15] >> 32
+s[:, 15] &= 0xffffffff
 wt = np.maximum(wit_tail, 1)
 print("after the drain, all waves: cycles per tail iteration refill+shading+step / MLP / scene:",
       np.round(tl.sum(axis=0) / wt.sum(), 0).tolist(), f" iterations with <= 4 rays: {int(s[:, 15].sum())} of {int(wit_tail.sum())}")
 for i in last[-3:]:
     print(f"  wave ending {end[i]:.1f} us: tail cycles/iter other {tl[i,0]/wt[i]:.0f} mlp {tl[i,1]/wt[i]:.0f} scene {tl[i,2]/wt[i]:.0f}; "
           f"iterations with <= 4 rays {int(s[i, 15])} of {int(wit_tail[i])}")
+print(f"live rays at the drain: total {int(nl_drain.sum())}, per wave p10/50/90/max",
+      np.percentile(nl_drain, [10, 50, 90, 100]).tolist(), f"; ray-steps after the drain {int(tail_steps.sum())}")
+if a.out:
+    np.savez_compressed(a.out, start=start, empty=empty, end=end, wit=wit, wit_tail=wit_tail, nl_drain=nl_drain,
+                        tail_steps=tail_steps, phases=ph, tail_phases=tl)
