@@ -265,8 +265,9 @@ int nr_set_debug(nr_ctx *ctx, int flags);
  * 16-bit march.  It needs the network's fp32x3 pack (the 7-hidden-layer [3|4, 32..., 1] shape whose
  * scales fit, as for the fp32x3 normals) and is off with nr_set_debug bit 15 (fp32 normals); the
  * wavefront and layered schedules march in pure 16-bit.  nr_stats.endgame_evals counts the fp32x3
- * evaluations. */
-#define NR_ENDGAME_DEFAULT 0.001f
+ * evaluations.  The default (round 5): the smallest threshold measured to hold
+ * every C3-C5 crop's coverage IoU against the exact-MLP frame at >= 0.997 (1e-4 left C4 at 0.993). */
+#define NR_ENDGAME_DEFAULT 0.0003f
 int nr_set_endgame(nr_ctx *ctx, float tau);
 /* Temporal scheduling: each launch (a frame, or a batch's launch of up to 32 frames)
  * records its 8x8 pixel blocks' longest ray (the max over the batch's frames) and the next

@@ -102,13 +102,16 @@ def contract(name, geom, size, steps, prec, rows, chrome, record, tau=0.0):
 
 # (identical, IoU, max per-channel mean |delta|) against the exact-MLP frame
 EXACT_BOUND = {"bf16": (0.72, 0.90, 12.0), "fp16": (0.75, 0.78, 3.6)}
-# with the endgame at NR_ENDGAME_DEFAULT (round 5, profiles/r5_lowp_contract.json): coverage IoU to
+# with the endgame at NR_ENDGAME_DEFAULT = 3e-4 (round 5, profiles/r5_lowp_contract.json): coverage IoU to
 # VERDICT r4's targets, identical pixels and mean |delta| within 2 points / 1.25x of the measured
 EG_IOU_TARGET = {"C3": 0.99, "C4": 0.99, "C5": 0.98}
-EXACT_EG_R5 = {("C3", "car_1"): (0.7795, 0.99997, 2.082), ("C4", "plane_2"): (0.8921, 0.99935, 4.5724),
-               ("C5", "plane_1"): (0.9017, 0.99892, 2.3629), ("C5", "plane_2"): (0.9324, 0.99991, 2.1207),
-               ("C5", "plane_3"): (0.9961, 0.99865, 0.982), ("C5", "car_1"): (0.7726, 0.99993, 1.9887),
-               ("C5", "3a3d4a90a2db90b4203936772104a82d.obj"): (0.8832, 0.99934, 2.1852)}
+EXACT_EG_R5 = {("C3", "car_1"): (0.7775, 0.99986, 2.2983),
+               ("C4", "plane_2"): (0.8843, 0.99827, 6.37),
+               ("C5", "plane_1"): (0.901, 0.99713, 2.3742),
+               ("C5", "plane_2"): (0.9316, 0.99984, 2.1632),
+               ("C5", "plane_3"): (0.9961, 0.99776, 0.9795),
+               ("C5", "car_1"): (0.7725, 0.9998, 1.99),
+               ("C5", "3a3d4a90a2db90b4203936772104a82d.obj"): (0.8824, 0.99815, 2.2141)}
 EXACT_R4 = {("C3", "car_1"): (0.7398, 0.99801, 5.629), ("C4", "plane_2"): (0.8367, 0.93107, 10.447),
             ("C5", "plane_1"): (0.8543, 0.86754, 3.266), ("C5", "plane_2"): (0.9205, 0.97787, 2.978),
             ("C5", "plane_3"): (0.9922, 0.81736, 1.412), ("C5", "car_1"): (0.7634, 0.99674, 2.687),
