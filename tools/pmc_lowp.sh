@@ -4,7 +4,8 @@
 # limits (8 SQ + 1 GRBM), with --kernel-trace for the dispatch durations.
 #   pass A: matrix-pipe busy, instruction mix, issue stalls (tools/pmc_mfma_summary.py)
 #   pass B: LDS instructions, bank-conflict and LDS-array cycles, LDS issue stalls, SALU
-# GPU box:  bash tools/pmc_lowp.sh OUTDIR [precision] [bpc]
+# GPU box:  bash tools/pmc_lowp.sh OUTDIR [precision] [bpc]   (EG=tau: the tracer's endgame threshold,
+# default 0 = the pure 16-bit march, so that the counters stay comparable with round 4's)
 set -e
 OUT=$(realpath -m "$1"); PREC=${2:-bf16}; BPC=${3:-3}
 REPO=$(cd "$(dirname "$0")/.." && pwd)
@@ -17,6 +18,6 @@ for pass in A B; do
     timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-trace --output-format csv -d "$OUT/mlp_$pass" -o run -- \
         python3 "$REPO/tools/mlp_bench.py" --n 16777216 --iters 3 --precision "$PREC" --bpc "$BPC" > "$OUT/mlp_$pass.log" 2>&1
     timeout -s KILL 120 rocprofv3 --pmc $CTR --kernel-trace --output-format csv -d "$OUT/trace_$pass" -o run -- \
-        python3 "$REPO/tools/render_frames.py" --frames 2 --batch 32 --precision "$PREC" > "$OUT/trace_$pass.log" 2>&1
+        python3 "$REPO/tools/render_frames.py" --frames 2 --batch 32 --precision "$PREC" --endgame "${EG:-0}" > "$OUT/trace_$pass.log" 2>&1
 done
 python3 "$REPO/tools/pmc_lowp_summary.py" "$OUT"

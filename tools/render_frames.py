@@ -1,6 +1,6 @@
 """Profiling driver: renders the benchmark workload for rocprofv3 runs.
 
-    python tools/render_frames.py [--frames 3] [--batch 0] [--precision fp32] [--temporal 0] [--bpc 0]
+    python tools/render_frames.py [--frames 3] [--batch 0] [--precision fp32] [--temporal 0] [--bpc 0] [--endgame T]
 --batch B > 0 renders each of the --frames launches as one nr_render_batch of B frames
 (the bench's batched kernel) into device buffers.
 """
@@ -20,6 +20,7 @@ ap.add_argument("--steps", type=int, default=128)
 ap.add_argument("--temporal", type=int, default=0)
 ap.add_argument("--bpc", type=int, default=0)
 ap.add_argument("--schedule", default="persistent")
+ap.add_argument("--endgame", type=float, default=-1.0, help="nr_set_endgame threshold (-1: the library's default)")
 a = ap.parse_args()
 if a.batch > 0:
     # torch's HIP state first, then libnr's (the other order breaks torch kernels under
@@ -29,6 +30,8 @@ if a.batch > 0:
 r = nr.Renderer(0).load_h5(nr.geometry_path("plane_1")).set_precision(a.precision)
 r.set_camera(0, 0, 2).set_static(1, 3).set_scene("v1").set_matcap(nr.load_png(nr.matcap_path("Chrome")))
 r.set_occupancy(a.bpc).set_temporal_order(a.temporal).set_schedule(a.schedule)
+if a.endgame >= 0:
+    r.set_endgame(a.endgame)
 if a.batch > 0:
     iv, nm = nr.camera(0, 0, 2)
     bufs = [torch.zeros(a.size * a.size, dtype=torch.int32, device="cuda") for _ in range(a.batch)]

@@ -205,6 +205,8 @@ def main():
         ("temporal bpc3", block_order(m, bmax), 3, False),
         ("spread16 merge", spread_order(m, 16), 2, True),
         ("spread16 bpc3 merge", spread_order(m, 16), 3, True),
+        ("spread16 share16", spread_order(m, 16), 2, 16),
+        ("spread16 share8", spread_order(m, 16), 2, 8),
         ("spread16 bpc3 share16", spread_order(m, 16), 3, 16),
         ("spread16 bpc3 share32", spread_order(m, 16), 3, 32),
     ]
