@@ -555,7 +555,7 @@ def main():
     # FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 corrections), per frame of this
     # workload, times the frames of one launch; bench.py cannot read PMC counters itself
     traffic, traffic_src = None, None
-    for name in ("r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json", "r1_pmc_traffic.json"):
+    for name in ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json", "r1_pmc_traffic.json"):
         try:
             tp = json.load(open(os.path.join(REPO, "profiles", name)))
         except (OSError, ValueError):
