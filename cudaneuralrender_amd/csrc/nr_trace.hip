@@ -611,14 +611,16 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             nstash -= nb;
         }
         NR_PHASE(fine);
-        // ---- EG: a fine pass over up to 64 rays of the fine queue (two 32-point tiles) whenever
-        // it holds a full tile -- repeated while it does -- and, once the pixel queue is drained,
-        // one per iteration (all of them when no coarse ray is left).  The stash holds fewer than
-        // SHR rays here and a pass adds at most 64 converged ones.
+        // ---- EG: a fine pass whenever the fine queue holds a full 32-point tile -- one tile (32
+        // rays) while it holds fewer than 64, two tiles from 64, repeated while it holds a tile --
+        // and, once the pixel queue is drained, one per iteration over up to 64 (all of them when
+        // no coarse ray is left).  (Passes of 33-63 rays on two tiles: C3 / C5 batch 2-9 % slower,
+        // profiles/r5_ab_eg.txt.)  The stash holds fewer than SHR rays here and a pass adds at
+        // most 64 converged ones.
         if constexpr (EG) {
             if (nfq >= 32 || (drained && nfq > 0 && (!lm || !fpass))) {
                 fpass = true;
-                const int nb = min(64, nfq);
+                const int nb = !drained && nfq < 64 ? 32 : min(64, nfq);
                 const int base = nfq - nb;
                 const bool act = lane < nb;
                 const int e = base + (act ? lane : 0);
