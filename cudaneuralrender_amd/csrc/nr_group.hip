@@ -264,7 +264,8 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
                 hipSuccess)
                 return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "copy to host");
     }
-    if (!(g->flags & NR_GROUP_ASYNC)) {
+    // host outputs are the caller's pageable memory: such a call returns with them written
+    if (!(g->flags & NR_GROUP_ASYNC) || loc != NR_DEVICE) {
         const int s = nr_group_synchronize(g);
         if (s != NR_OK) return s;
     }

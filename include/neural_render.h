@@ -190,8 +190,9 @@ int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out);
  * layout and re-interleave; contexts may then share a GPU -- how a one-GPU box runs multi-rank
  * groups); NR_GROUP_ASYNC returns once the call's gather and re-interleave are enqueued on the
  * group's communication streams, so the next call's render overlaps this call's transfer (shard
- * and gather buffers are double-buffered): frames[i].out of a call is complete after
- * nr_group_synchronize -- or, without the flag, when the call returns. */
+ * and gather buffers are double-buffered): frames[i].out of an NR_DEVICE call is complete after
+ * nr_group_synchronize -- or, without the flag, when the call returns.  A call with host outputs
+ * (loc != NR_DEVICE) always returns with its frames written. */
 #define NR_GROUP_COPY 1
 #define NR_GROUP_ASYNC 2
 int nr_group_create_ex(nr_ctx *const *ctxs, int n, int flags, nr_group **out);

@@ -109,6 +109,25 @@ def test_group_async_calls_overlap_and_stay_exact(chrome):
             r.close()
 
 
+def test_group_async_host_outputs_are_complete_on_return(chrome):
+    """NR_GROUP_ASYNC with host outputs: the call returns with the frames written (no
+    nr_group_synchronize needed), call after call."""
+    n = min(max(NGPU, 2), 3)
+    devs = list(range(n)) if NGPU >= n else [0] * n
+    rs = [_setup(nr.Renderer(d), "fp32", chrome) for d in devs]
+    calls = [[(*nr.camera(9.0 * k, 30.0 * k + 7 * i, 2.0), k) for i in range(2)] for k in range(3)]
+    try:
+        with nr.Group(rs, copy=NGPU < n, asynchronous=True) as g:
+            for cams in calls:
+                imgs, _ = g.render_batch(128, 80, cams, 96, band=1)
+                refs = _refs(rs[0], cams, 128, 80, 96)
+                for a, b in zip(imgs, refs):
+                    assert np.array_equal(a, b[0])
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_group_rejects_two_contexts_on_one_gpu_without_copy():
     with nr.Renderer(0) as a, nr.Renderer(0) as b:
         with pytest.raises(nr.NRError):
