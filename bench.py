@@ -320,15 +320,28 @@ def group_child(a):
         "parallelism": d["config"]["parallelism"], "roofline_frac_gpu0": d["roofline"]["frac"]}
 
 
+def json_stdout():
+    """The bench's stdout carries its one JSON line only: native libraries that write to fd 1
+    (RCCL's version banner at communicator set-up, ...) are pointed at stderr, and the JSON line
+    goes to a private copy of the real stdout.  Called in the process that prints the line (not
+    in a launcher whose children inherit fd 1)."""
+    sys.stdout.flush()
+    real = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(real, "w", buffering=1)
+
+
 def main():
     a = parse()
     if a.group:
         if "WORLD_SIZE" in os.environ:
             raise SystemExit("--group runs in one process: start it without torch.distributed.run")
-        print(json.dumps(main_group(a)), flush=True)
+        out = json_stdout()
+        print(json.dumps(main_group(a)), file=out, flush=True)
         return
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(self_launch(a))
+    jout = json_stdout()
     import torch
     import torch.distributed as dist
     import cudaneuralrender_amd as nr
@@ -659,7 +672,7 @@ def main():
     }
     if world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(size, a.max_steps, a.cpu_threads, geometry, matcap, iv, nm)
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=jout, flush=True)
     if world > 1:
         dist.destroy_process_group()
 
