@@ -589,7 +589,9 @@ def main():
         torch.cuda.synchronize()
         if rank == 0:
             group = group_child(a)
-        dist.barrier()
+        # on the CPU (gloo): an RCCL barrier would leave a spinning collective kernel on every other
+        # GPU while the child renders there
+        dist.barrier(group=status_group(dist))
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
