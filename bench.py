@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--no-fp32x3", action="store_true",
                     help="skip config.fp32x3 (the same frames timed in NR_PRECISION_FP32X3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="take roofline.traffic from the committed PMC figure instead of two rocprofv3 --pmc "
+                         "child passes in this run")
     ap.add_argument("--no-single-frame", action="store_true")
     ap.add_argument("--no-spin", action="store_true",
                     help="skip config.spin (the reference's --spin sequence, one launch per frame)")
@@ -149,6 +152,58 @@ def cpu_baseline(size, max_steps, threads, geometry, matcap, iv, nm):
             "host_logical_cpus": os.cpu_count(),
             "threads_note": "the GPU box's CPU share is 16 threads (OMP_NUM_THREADS); os.cpu_count() "
                             "reports the whole machine"}
+
+
+def live_traffic(frames, precision, size, max_steps):
+    """k_trace's HBM bytes per launch measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE,
+    then WRITE_SIZE -- separate runs, MI355X_MICROARCH.md's HBM/rocprofv3 recipe) over
+    tools/render_frames.py rendering 3 launches of the bench's batch (`frames` frames of the same
+    workload per nr_render_batch), each pass a child process under a hard time limit.  gfx950
+    corrections: FETCH_SIZE is KiB and under-counts wide reads 2x, WRITE_SIZE is KiB.  Returns
+    (bytes per launch, detail) or None when rocprofv3 is absent or a pass fails (the caller then
+    falls back to the committed figure)."""
+    import csv
+    import glob
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None or "ROCPROF_OUTPUT_PATH" in os.environ:   # absent, or this run is itself profiled
+        return None
+    kname = "k_trace<0, false, false, true, false, false>"
+    tmp = tempfile.mkdtemp(prefix="nr_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    t0 = time.perf_counter()
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            cmd = ["timeout", "-k", "5", "-s", "KILL", "90", prof, "--pmc", counter, "--output-format", "csv",
+                   "-d", os.path.join(tmp, counter), "-o", "run", "--", sys.executable,
+                   os.path.join(REPO, "tools", "render_frames.py"), "--frames", "3", "--batch", str(frames),
+                   "--precision", precision, "--size", str(size), "--steps", str(max_steps)]
+            with open(os.path.join(tmp, counter + ".log"), "w") as log:
+                rc = subprocess.run(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
+                                    timeout=120).returncode
+            got = []
+            for f in glob.glob(os.path.join(tmp, counter, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    got += [float(r["Counter_Value"]) for r in csv.DictReader(fh)
+                            if kname in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if rc != 0 or not got:
+                print(f"bench: live PMC pass {counter} failed (exit {rc}, {len(got)} dispatches); "
+                      "using the committed traffic figure", file=sys.stderr)
+                return None
+            vals[counter] = (sum(got) / len(got), len(got))
+    except (OSError, subprocess.SubprocessError) as e:
+        print(f"bench: live PMC passes unavailable ({e}); using the committed traffic figure", file=sys.stderr)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch, write = vals["FETCH_SIZE"][0], vals["WRITE_SIZE"][0]
+    hbm = fetch * 1024 * 2 + write * 1024
+    return int(hbm), {"fetch_size_kb": round(fetch, 2), "write_size_kb": round(write, 2),
+                      "dispatches": [vals["FETCH_SIZE"][1], vals["WRITE_SIZE"][1]],
+                      "frames_per_launch": frames, "seconds": round(time.perf_counter() - t0, 1),
+                      "algorithmic_bytes_per_launch": size * size * 4 * frames + 30 * 1024 + 1024 * 1024}
 
 
 def random_poses(n=8):
@@ -567,7 +622,7 @@ def main():
     # HBM traffic of k_trace from the PMC pass committed under profiles/ (rocprofv3 --pmc
     # FETCH_SIZE / WRITE_SIZE, separate passes, gfx950 corrections), per frame of this
     # workload, times the frames of one launch; bench.py cannot read PMC counters itself
-    traffic, traffic_src = None, None
+    traffic, traffic_src, traffic_live = None, None, None
     for name in ("r5_pmc_traffic.json", "r4_pmc_traffic.json", "r3_pmc_traffic.json", "r2_pmc_traffic.json", "r1_pmc_traffic.json"):
         try:
             tp = json.load(open(os.path.join(REPO, "profiles", name)))
@@ -581,6 +636,13 @@ def main():
                 traffic = int(per_frame * min(a.steps, MAX_BATCH))
                 traffic_src = name
         break
+    # ... or measured in this run: two rocprofv3 --pmc child passes over the same batched launch
+    if (a.config == "c2" and a.precision == "fp32" and world == 1 and not a.no_live_traffic
+            and min(a.steps, MAX_BATCH) == a.steps):
+        torch.cuda.synchronize()
+        live = live_traffic(a.steps, a.precision, size, a.max_steps)
+        if live is not None:
+            traffic, traffic_live = live
 
     # the C-ABI multi-GPU path (nr_group) over the same N GPUs, in a child of rank 0, after every
     # timed region; the other ranks wait at the barrier (their contexts stay idle meanwhile)
@@ -661,8 +723,12 @@ def main():
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "traffic": traffic,
-            "traffic_unit": f"HBM bytes per launch (per-frame PMC figure x frames per launch, profiles/{traffic_src})"
-                            if traffic is not None else None,
+            "traffic_unit": ("HBM bytes per launch, measured in this run (rocprofv3 --pmc FETCH_SIZE and "
+                             "WRITE_SIZE child passes over the same batched launch; FETCH_SIZE KiB x 2 + "
+                             "WRITE_SIZE KiB, gfx950 corrections)" if traffic_live is not None else
+                             f"HBM bytes per launch (per-frame PMC figure x frames per launch, profiles/{traffic_src})"
+                             if traffic is not None else None),
+            "traffic_live": traffic_live,
             "flop_per_launch": round(flop_per_launch, 1),
             "avg_launch_ms": round(march_avg_ms, 5),
             "launches": int(prof["march_launches"]),

@@ -14,7 +14,7 @@ mkdir -p "$OUT"
 timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ktrace" -o run -- \
-    python3 "$REPO/bench.py" --no-cpu-baseline --no-single-frame --no-random-poses --warmup 32 > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err"
+    python3 "$REPO/bench.py" --no-cpu-baseline --no-live-traffic --no-single-frame --no-random-poses --warmup 32 > "$OUT/ktrace_bench.json" 2> "$OUT/ktrace.err"
 # the PMC passes drive the bench's batched kernel (32 frames per launch, bench default)
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
     python3 "$REPO/tools/render_frames.py" --frames 3 --batch 32 > "$OUT/fetch.log" 2>&1
