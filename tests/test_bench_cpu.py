@@ -1,6 +1,7 @@
 """bench.py's host logic on CPU: the --gpus N self-launch (no launcher in the environment)
 and the pose list.  No GPU is touched: the launcher is stubbed."""
 import os
+import shutil
 import subprocess
 import sys
 
@@ -69,3 +70,59 @@ def test_c5_rank_geometries():
     g = [bench.GEOMS[r % len(bench.GEOMS)] for r in range(8)]
     assert g[:5] == bench.GEOMS and g[5:] == bench.GEOMS[:3]
     assert all(os.path.exists(os.path.join(REPO, "data", "neuralGeometries", x + ".h5")) for x in bench.GEOMS)
+
+
+def _fake_rocprof(monkeypatch, values, rc=0):
+    """Stub of the two rocprofv3 --pmc child runs: each writes a counter_collection.csv holding
+    `values[counter]` per k_trace dispatch (plus a dispatch of another kernel) under its -d directory."""
+    calls = []
+
+    def fake_run(cmd, cwd=None, env=None, stdout=None, stderr=None, timeout=None):
+        calls.append(cmd)
+        counter = cmd[cmd.index("--pmc") + 1]
+        out = os.path.join(cmd[cmd.index("-d") + 1], "host", "1")
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, "run_counter_collection.csv"), "w") as f:
+            f.write("Kernel_Name,Counter_Name,Counter_Value\n")
+            for v in values.get(counter, []):
+                f.write(f"\"void nr::k_trace<0, false, false, true, false, false>(RenderArgs, MlpArgs, TraceArgs)\",{counter},{v}\n")
+            f.write(f"k_assemble,{counter},999999\n")
+        return subprocess.CompletedProcess(cmd, rc)
+
+    monkeypatch.setattr(shutil, "which", lambda name: "/opt/rocm/bin/rocprofv3")
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.delenv("ROCPROF_OUTPUT_PATH", raising=False)
+    return calls
+
+
+def test_live_traffic_applies_gfx950_corrections(monkeypatch):
+    """roofline.traffic measured in the run: FETCH_SIZE (KiB, wide reads under-counted 2x) and
+    WRITE_SIZE (KiB) from two separate --pmc passes, averaged over the k_trace dispatches only."""
+    calls = _fake_rocprof(monkeypatch, {"FETCH_SIZE": [5000, 5100, 5200], "WRITE_SIZE": [230000, 231000, 232000]})
+    got = bench.live_traffic(32, "fp32", 1024, 128)
+    assert got is not None
+    hbm, detail = got
+    assert hbm == int(5100 * 1024 * 2 + 231000 * 1024)
+    assert detail["dispatches"] == [3, 3] and detail["frames_per_launch"] == 32
+    assert detail["algorithmic_bytes_per_launch"] == 1024 * 1024 * 4 * 32 + 30 * 1024 + 1024 * 1024
+    # two passes, one counter each, the program itself after "--" (no shell or env hop under the profiler)
+    assert [c[c.index("--pmc") + 1] for c in calls] == ["FETCH_SIZE", "WRITE_SIZE"]
+    for c in calls:
+        assert c[c.index("--") + 1] == sys.executable
+        assert sum(x.startswith("-") and "trace" in x for x in c) == 0   # counters only, no trace domain
+        assert c[:2] == ["timeout", "-k"]
+
+
+def test_live_traffic_falls_back(monkeypatch):
+    """A failed pass, a pass with no k_trace dispatch, a profiled parent or no rocprofv3: None (the
+    caller then reports the committed figure)."""
+    _fake_rocprof(monkeypatch, {"FETCH_SIZE": [5000], "WRITE_SIZE": [230000]}, rc=124)
+    assert bench.live_traffic(32, "fp32", 1024, 128) is None
+    _fake_rocprof(monkeypatch, {"FETCH_SIZE": [5000]})
+    assert bench.live_traffic(32, "fp32", 1024, 128) is None
+    _fake_rocprof(monkeypatch, {"FETCH_SIZE": [5000], "WRITE_SIZE": [230000]})
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+    assert bench.live_traffic(32, "fp32", 1024, 128) is None
+    monkeypatch.delenv("ROCPROF_OUTPUT_PATH")
+    monkeypatch.setattr(shutil, "which", lambda name: None)
+    assert bench.live_traffic(32, "fp32", 1024, 128) is None
