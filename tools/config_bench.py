@@ -24,7 +24,7 @@ import torch  # noqa: E402
 
 import cudaneuralrender_amd as nr  # noqa: E402
 
-PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6}
+PEAK = {"fp32": 157.3, "bf16": 2516.6, "fp16": 2516.6, "fp32x3": 2516.6}
 FLOP = 14592
 ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=10)
@@ -46,7 +46,7 @@ def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1, tau=No
            "Mray_steps_per_s": round(rs / t / 1e3, 1),
            "TFLOPs": round(evals * FLOP / t / 1e9, 2),
            "frac_of_peak": round(evals * FLOP / t / 1e9 / PEAK[prec], 4)}
-    if prec != "fp32":
+    if prec in ("bf16", "fp16"):
         res["endgame_tau"] = tau
         res["fp32x3_share"] = round(st.get("endgame_evals", 0) / max(st["ray_steps"], 1), 4)
     print(json.dumps(res), flush=True)
@@ -55,7 +55,7 @@ def report(name, geom, size, prec, steps, shard, sched, t, st, nframes=1, tau=No
 def run(name, geom, size, prec, steps, shard=None):
     if a.only and name not in a.only.split(","):
         return
-    taus = [float(t) for t in a.endgame.split(",")] if a.endgame and prec != "fp32" else [None]
+    taus = [float(t) for t in a.endgame.split(",")] if a.endgame and prec in ("bf16", "fp16") else [None]
     for tau in taus:
         run1(name, geom, size, prec, steps, shard, tau)
 
@@ -92,6 +92,8 @@ def run1(name, geom, size, prec, steps, shard, tau):
 
 run("C3", "car_1", 2048, "bf16", 256)
 run("C3-fp32", "car_1", 2048, "fp32", 256)
+# the endgame's fine arithmetic on every evaluation (what a fine pass costs against the bulk form)
+run("C3-fp32x3", "car_1", 2048, "fp32x3", 256)
 run("C4-full", "plane_2", 4096, "bf16", 128)
 run("C4-shard0of8", "plane_2", 4096, "bf16", 128, shard=0)
 for g in ["plane_1", "plane_2", "plane_3", "car_1", "3a3d4a90a2db90b4203936772104a82d.obj"]:
