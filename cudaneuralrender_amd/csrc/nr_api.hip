@@ -55,11 +55,6 @@ struct nr_ctx {
     bool f32_clamp_ok = false;  // the fp32 pack is scaled for the clamped ReLU (pack_fp32_16)
     int schedule = 0; // NR_SCHED_PERSISTENT
     uint32_t *d_tr = nullptr;  // persistent-schedule counters + stats
-    // the endgame's hand-off buffer (TraceArgs::ho_*): 24 bytes per slot, grown on demand
-    float4 *d_ho_p = nullptr;
-    uint2 *d_ho_q = nullptr;
-    uint32_t *d_ho_ctr = nullptr;
-    size_t ho_cap = 0;
     int debug = 0;
     int blocks_per_cu = 0;     // persistent grid: blocks (4 waves) per CU; 0 = auto
     // temporal block ordering (nr_set_temporal_order)
@@ -205,7 +200,6 @@ int upload_lowp(nr_ctx *c) {
     c->mlp16.lp_clamp = 0;
     dfree(c->d_x3lp); dfree(c->d_x3fl);
     c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
-    c->mlp16.x3lp_bytes = 0; c->mlp16.x3fl_bytes = 0;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
@@ -234,7 +228,6 @@ int upload_lowp(nr_ctx *c) {
         MlpArgs X{};
         if ((rc = upload_pack(c, xa, xf, c->d_x3lp, c->d_x3fl, X)) != NR_OK) return rc;
         c->mlp16.x3lp = X.lp; c->mlp16.x3fl = X.lpf;
-        c->mlp16.x3lp_bytes = X.lp_bytes; c->mlp16.x3fl_bytes = X.lpf_bytes;
         c->mlp16.x3n = c->fp32_normals ? 0 : 1;
     }
     return NR_OK;
@@ -350,29 +343,6 @@ int read_queue_counters(nr_ctx *c, int max_steps, nr_stats &st, hipStream_t s);
 static float endgame_tau(const nr_ctx *c, int max_steps) {
     const bool lowp = c->precision == NR_PRECISION_BF16 || c->precision == NR_PRECISION_FP16;
     return lowp && c->mlp16.x3n && max_steps < (1 << 24) ? c->eg_tau : 0.0f;
-}
-
-// The endgame's hand-off slots for a launch of `rays` pixels on `grid` workgroups: every ray is
-// handed off at most once, and each wave leaves fewer than 64 reserved slots unused.  Grown on
-// demand (after the stream's earlier launches are done with the old buffer).
-static int handoff_buffers(nr_ctx *c, TraceArgs &T, size_t rays, int grid, hipStream_t s) {
-    if (T.eg_tau <= 0.0f) return NR_OK;
-    const size_t need = rays + (size_t)grid * 4 * 64;
-    if (need > 0xffffffffull) return set_err(c, NR_E_INVALID, "endgame: %zu hand-off slots overflow 32 bits", need);
-    if (need > c->ho_cap) {
-        HIPCHK(c, hipStreamSynchronize(s));
-        dfree(c->d_ho_p); dfree(c->d_ho_q);
-        c->ho_cap = 0;
-        HIPCHK(c, hipMalloc(&c->d_ho_p, need * sizeof(float4)));
-        HIPCHK(c, hipMalloc(&c->d_ho_q, need * sizeof(uint2)));
-        c->ho_cap = need;
-    }
-    if (!c->d_ho_ctr) HIPCHK(c, hipMalloc(&c->d_ho_ctr, 256));
-    T.ho_p = c->d_ho_p;
-    T.ho_q = c->d_ho_q;
-    T.ho_ctr = c->d_ho_ctr;
-    T.ho_cap = (uint32_t)c->ho_cap;
-    return NR_OK;
 }
 
 // Persistent-tracer workgroups per CU for a launch of `total` pixels over `nframes` frames
@@ -778,7 +748,7 @@ int nr_destroy(nr_ctx *c) {
     if (!(c->use_own && !c->own_stream)) (void)hipStreamSynchronize(c->stream);
     free_network(c);
     for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
-    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_ho_p); dfree(c->d_ho_q); dfree(c->d_ho_ctr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
+    dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
     dfree(c->d_frames); dfree(c->d_bout);
     if (c->h_frames) (void)hipHostFree(c->h_frames);
@@ -1007,7 +977,6 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
             HIPCHK(c, hipMemsetAsync(c->d_bcost, 0, (size_t)T.nblocks * 4, s));
         }
         int rc2;
-        if ((rc2 = handoff_buffers(c, T, npix * n, grid, s)) != NR_OK) return rc2;
         if ((rc2 = prof_begin(c, 1, s)) != NR_OK) return rc2;
         HIPCHK(c, launch_trace(A, mlp_for_frames(c, frames, nframes, 0), T, c->precision, grid, s));
         if ((rc2 = prof_end(c, s)) != NR_OK) return rc2;
@@ -1142,7 +1111,6 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         if (grid < 1) grid = 1;
         T.take = wave_rays_for(c, npix, grid);
         T.lane_cap = T.take >= 64 ? ~0ull : (1ull << T.take) - 1ull;
-        if ((rc2 = handoff_buffers(c, T, npix, grid, s)) != NR_OK) return rc2;
         if (c->debug & 1) {
             if (!c->d_stamps) HIPCHK(c, hipMalloc(&c->d_stamps, (size_t)cus * 16 * 4 * 16 * 8));
             T.stamps = c->d_stamps;

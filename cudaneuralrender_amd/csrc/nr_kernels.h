@@ -22,7 +22,6 @@ struct MlpArgs {
     const float *x3fl;
     int x3n;                // bf16/fp16: 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3
                             // (mlp16_x3_normal), 0 = in fp32
-    int x3lp_bytes, x3fl_bytes;  // sizes of the fp32x3 pack (k_fine stages it into LDS)
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,
@@ -117,16 +116,7 @@ struct TraceArgs {
     double inv_nframes;         // 1 / nframes for udiv_r
     float eg_tau;               // bf16/fp16 with an fp32x3 pack: the endgame's switch threshold (0 = off;
                                 // k_trace's EG instances, nr_set_endgame)
-    // the endgame's hand-off: k_trace's EG instance writes a ray whose 16-bit SDF fell below eg_tau
-    // here -- {p.xyz, tfar}, {pixel, iterations | frame << 24} -- and k_fine marches it on in fp32x3
-    // after the launch.  Slots are reserved 64 at a time per wave; a wave's unused slots are marked
-    // HO_EMPTY when it ends, so every slot below ho_ctr[0] holds a ray or HO_EMPTY.
-    float4 *ho_p;
-    uint2 *ho_q;
-    uint32_t *ho_ctr;           // [0] slots reserved (k_trace), [1] slots dealt (k_fine)
-    uint32_t ho_cap;            // slots allocated: the launch's pixels + 64 per wave
 };
-constexpr uint32_t HO_EMPTY = 0xffffffffu;
 
 int dense_lds_bytes(int in, int out);
 hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);

@@ -194,17 +194,22 @@ __device__ __forceinline__ void set_priority(int prio) {
 #endif
 // NX3: the bf16/fp16 instances whose normals are fp32x3 (MlpArgs::x3n; mlp16_x3_normal).
 // EG: the bf16/fp16 instances with the fp32x3 endgame (TraceArgs::eg_tau > 0, round 5): a marching
-// ray whose 16-bit MLP output falls below eg_tau leaves its lane without taking the step and is
-// handed off to global memory (TraceArgs::ho_*); after the launch k_fine marches the handed-off
-// rays in fp32x3 -- the fp32x3 MLP on their points (mlp16_x3_normal's per-point rule: the split
-// within the x3 pack's bounds, the fp32 MLP outside), the scene and singleMarch's step -- to their
-// end.  So the switch iteration's step, the convergence test (:474), the background test and every
-// later step of the ray are decided in fp32x3.  Oracle: nr_oracle.c or_set_endgame.
-// (Round 5's first form marched them in k_trace itself, through a per-wave LDS fine queue: its
-// fine pass needed 161 VGPRs -- 3 workgroups per CU -- and read the fp32x3 weights from global
-// memory, 1.96x the cost per evaluation of k_fine's form; profiles/r5_eg_cost.txt.)
+// ray whose 16-bit MLP output falls below eg_tau leaves its lane for the wave's fine queue in LDS
+// without taking the step; whenever the queue holds a full 32-point tile (or the pixel queue is
+// drained) the wave takes up to 64 queued rays through a fine pass -- the fp32x3 MLP on their
+// points (mlp16_x3_normal's per-point rule: the split within the x3 pack's bounds, the fp32 MLP
+// outside), the scene and singleMarch's step -- and returns the survivors to the queue.  So the
+// switch iteration's step, the convergence test (:474), the background test and every later step
+// of the ray are decided in fp32x3, on full tiles.  Oracle: nr_oracle.c or_set_endgame.
+// (3 workgroups per CU: the fine pass's registers -- 161 VGPRs; at 4 per CU, <= 128 VGPRs, the
+// spills cost C3 +25 %, C5 +40-55 %; a pass per 64 queued rays instead of 32: C5 batch +5-10 %;
+// profiles/r5_ab_eg.txt)
+#ifndef NR_TRACE_BPC_EG
+#define NR_TRACE_BPC_EG 3
+#endif
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false>
-__global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
+__global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
+                                  : PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                   : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
                                   : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
     constexpr int prec = PREC;
@@ -243,9 +248,14 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
     // each lane's marching ray {d.xyz, pixel} (DLDS): 4 KB per workgroup
     constexpr bool DLDS = DENSE && NR_RAY_D_LDS;
     __shared__ float4 ray_dp[DLDS ? 4 : 1][DLDS ? 64 : 1];
+    // EG: per wave the fine queue {p.xyz, tfar}, {d.xyz, pixel}, iteration | frame << 24: a pass
+    // leaves fewer than 32 rays (or none), one iteration adds at most 64
     static_assert(!EG || (DLDS && NX3 && (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16)), "EG instances");
-    // EG: the wave's reserved hand-off slots [ho_base, ho_base + ho_cnt)
-    uint32_t ho_base = 0, ho_cnt = 0;
+    constexpr int FQ = EG ? 32 - 1 + 64 : 1;
+    __shared__ float4 fq_p[EG ? 4 : 1][FQ], fq_d[EG ? 4 : 1][FQ];
+    __shared__ uint32_t fq_i[EG ? 4 : 1][FQ];
+    int nfq = 0;        // rays in the wave's fine queue (EG)
+    uint32_t nfine = 0;  // fp32x3 march evaluations (EG)
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -301,10 +311,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         pend = __builtin_amdgcn_readfirstlane((int)pend) != 0;
         rb_n = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_n);
         rb_head = (uint32_t)__builtin_amdgcn_readfirstlane((int)rb_head);
-        if constexpr (EG) {
-            ho_base = (uint32_t)__builtin_amdgcn_readfirstlane((int)ho_base);
-            ho_cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)ho_cnt);
-        }
+        if constexpr (EG) nfq = __builtin_amdgcn_readfirstlane(nfq);
         NR_PHASE(refill);
         // ---- refill free slots from the pixel queue
         if (!qempty || (DENSE && rb_n > 0)) {
@@ -561,7 +568,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[0] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         uint64_t lm = __ballot(it >= 0);
         constexpr int SHR = PREC == NR_PRECISION_FP32 ? 16 : NR_SHADE_RAYS_LOWP;  // rays per shading pass
-        while (nstash >= SHR || (drained && nstash > 0 && !lm)) {
+        bool fpass = false;  // EG: a fine pass ran in this iteration
+        while (true) {
+        while (nstash >= SHR || (drained && nstash > 0 && !lm && nfq == 0)) {
             const int nb = min(SHR, nstash);
             const int k = lane >> 2;
             const int e = nstash - nb + (k < nb ? k : 0);
@@ -601,9 +610,95 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             nconv += (uint32_t)nb;
             nstash -= nb;
         }
+        NR_PHASE(fine);
+        // ---- EG: a fine pass whenever the fine queue holds a full 32-point tile -- one tile (32
+        // rays) while it holds fewer than 64, two tiles from 64, repeated while it holds a tile --
+        // and, once the pixel queue is drained, one per iteration over up to 64 (all of them when
+        // no coarse ray is left).  (Passes of 33-63 rays on two tiles: C3 / C5 batch 2-9 % slower,
+        // profiles/r5_ab_eg.txt.)  The stash holds fewer than SHR rays here and a pass adds at
+        // most 64 converged ones.
+        if constexpr (EG) {
+            if (nfq >= 32 || (drained && nfq > 0 && (!lm || !fpass))) {
+                fpass = true;
+                const int nb = !drained && nfq < 64 ? 32 : min(64, nfq);
+                const int base = nfq - nb;
+                const bool act = lane < nb;
+                const int e = base + (act ? lane : 0);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                const float4 qp = fq_p[wid][e], qd = fq_d[wid][e];
+                const uint32_t qi = fq_i[wid][e];
+                F3 fp = mk3(qp.x, qp.y, qp.z);
+                float ftf = qp.w;
+                const uint32_t fpix = __float_as_uint(qd.w);
+                int fit = (int)(qi & 0xffffffu);
+                const int ff = BATCH ? (int)(qi >> 24) : 0;
+                // the fp32x3 pack's address made opaque, as in the shading pass
+                int zx = 0;
+                asm volatile("" : "+s"(zx));
+                // (one two-tile pass: C3 batch 1.85 -> 1.72 ms against two one-tile passes)
+                const float fsdf = mlp16_x3_normal<false>(M, S.s32, M.x3lp + zx, M.x3fl + zx, fr_of(ff), fp.x, fp.y, fp.z,
+                                                          nb > 32 ? 0xfu : 0x3u);
+                nfine += (uint32_t)nb;
+                nsteps += (uint32_t)nb;
+                bool fconv = false, keep = false;
+                if (act) {
+                    // singleMarch (:416-477) on the fp32x3 value, as the coarse step below
+                    const float ts = scene_sdf(fp, fsdf, A.scene, zoff_of(ff));
+                    ftf -= ts;
+                    int used = 0;
+                    if (ftf <= 0) {
+                        put(ff, fpix, 0u);
+                        used = fit + 1;
+                    } else {
+                        fp = add3(fp, mul3s(mk3(qd.x, qd.y, qd.z), ts));
+                        if (ts < MARCHING_EPSILON) {
+                            if (fit + 1 < A.max_steps) {
+                                fconv = true;
+                                used = fit + 2;
+                            } else {
+                                put(ff, fpix, 0u);
+                                used = fit + 1;
+                            }
+                        } else if (++fit >= A.max_steps) {
+                            put(ff, fpix, 0u);
+                            used = A.max_steps;
+                        }
+                    }
+                    if (used) {
+                        maxit = max(maxit, used);
+                        if (T.itmap) put(ff, fpix, (uint32_t)used);
+                        if (T.bcost) {
+                            const int yy = (int)(fpix / (uint32_t)A.W), xx = (int)(fpix - (uint32_t)yy * A.W);
+                            atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
+                        }
+                    } else {
+                        keep = true;
+                    }
+                }
+                // survivors back to the queue (positions [base, base + survivors)), converged rays
+                // to the stash
+                const uint64_t km = __ballot(keep), cm = __ballot(fconv);
+                if (keep) {
+                    const int slot = base + (int)rank_below(km);
+                    fq_p[wid][slot] = make_float4(fp.x, fp.y, fp.z, ftf);
+                    fq_d[wid][slot] = qd;
+                    fq_i[wid][slot] = (uint32_t)fit | ((uint32_t)ff << 24);
+                }
+                if (fconv) {
+                    const int slot = nstash + (int)rank_below(cm);
+                    stash[wid][slot] = make_float4(fp.x, fp.y, fp.z, __uint_as_float(fpix));
+                    if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)ff;
+                }
+                nstash += (int)__popcll(cm);
+                nfq = base + (int)__popcll(km);
+                continue;
+            }
+        }
+        break;
+        }
         if constexpr (timing) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph[1] += t - tph; pt[0] += drained ? t - tph : 0; tph = t; }
         if (!lm) {
-            if (drained && nstash == 0) break;
+            if (drained && nstash == 0 && nfq == 0) break;
             continue;
         }
         uint32_t tmask = tiles_of(lm);
@@ -654,38 +749,27 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
             if (lane == 0) atomicAdd(T.stats + 0, (unsigned long long)nsteps);
             nsteps = 0;
         }
+        if (EG && nfine >= (1u << 30)) {
+            if (lane == 0) atomicAdd(T.stats + 4, (unsigned long long)nfine);
+            nfine = 0;
+        }
         ++wit;
         wit_tail += drained ? 1u : 0u;
         bool conv = false;
         if constexpr (EG) {
-            // the endgame's switch: the ray is handed off without taking the step (k_fine
-            // re-evaluates this point in fp32x3); its lane is free for a new ray.  Slots come from
-            // the wave's reservation, 64 more (one atomic) when it runs short: n - r <= 64.
+            // the endgame's switch: the ray goes to the fine queue without taking the step (the
+            // fine pass re-evaluates this point in fp32x3); its lane is free for a new ray
             const bool hand = it >= 0 && sdf < T.eg_tau;
             const uint64_t hm = __ballot(hand);
             if (hm) {
-                const uint32_t n = (uint32_t)__popcll(hm), r = min(n, ho_cnt);
-                const uint32_t base1 = ho_base;
-                uint32_t base2 = 0;
-                ho_base += r;
-                ho_cnt -= r;
-                if (n > r) {
-                    uint32_t b = 0;
-                    if (lane == 0) b = atomicAdd(T.ho_ctr, 64u);
-                    base2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-                    ho_base = base2 + (n - r);
-                    ho_cnt = 64u - (n - r);
-                }
                 if (hand) {
-                    const uint32_t k = rank_below(hm);
-                    const uint32_t slot = k < r ? base1 + k : base2 + (k - r);
-                    if (slot < T.ho_cap) {  // (never reached: ho_cap covers every ray + 64 per wave)
-                        const float4 dp = ray_dp[wid][lane];
-                        T.ho_p[slot] = make_float4(p.x, p.y, p.z, tfar);
-                        T.ho_q[slot] = make_uint2(__float_as_uint(dp.w), (uint32_t)it | ((uint32_t)rf << 24));
-                    }
+                    const int slot = nfq + (int)rank_below(hm);
+                    fq_p[wid][slot] = make_float4(p.x, p.y, p.z, tfar);
+                    fq_d[wid][slot] = ray_dp[wid][lane];
+                    fq_i[wid][slot] = (uint32_t)it | ((uint32_t)rf << 24);
                     it = -1;
                 }
+                nfq += (int)__popcll(hm);
             }
         }
         if (it >= 0) {
@@ -758,9 +842,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
         if (nhit) atomicAdd(T.stats + 1, (unsigned long long)nhit);
         if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
         if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
-    }
-    if constexpr (EG) {  // the wave's unused hand-off slots
-        if ((uint32_t)lane < ho_cnt && ho_base + (uint32_t)lane < T.ho_cap) T.ho_q[ho_base + lane] = make_uint2(0u, HO_EMPTY);
+        if (EG && nfine) atomicAdd(T.stats + 4, (unsigned long long)nfine);
     }
 }
 
@@ -1020,179 +1102,6 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
     return hipSuccess;
 }
 
-// The endgame's fine march (round 5): k_fine takes the rays k_trace's EG instance handed off
-// (TraceArgs::ho_*) and marches each to its end in fp32x3 -- every evaluation mlp16_x3_normal's
-// per-point rule (the split within the fp32x3 pack's bounds, the fp32 MLP outside), then
-// singleMarch's step (:416-477) exactly as k_trace takes it, converged rays coloured with fp32x3
-// normals as k_trace's NX3 shading does.  A ray's values depend on nothing but the ray, so the
-// frames equal the oracle's endgame (or_set_endgame) bit for bit whichever kernel marches what.
-// Persistent waves over the hand-off buffer: free lanes take the next slots (one atomic per
-// refill), the fp32x3 pack sits in LDS (k_trace's workgroups hold the 16-bit pack there), the
-// fp32 pack for out-of-bound points stays in global memory.  The ray direction is regenerated
-// from the pixel (ray_dir, as the facing colour does), so a slot is 24 bytes.
-#ifndef NR_FINE_BPC
-#define NR_FINE_BPC 3
-#endif
-template <bool BATCH>
-__global__ __launch_bounds__(256, NR_FINE_BPC) void k_fine(RenderArgs A, MlpArgs M, TraceArgs T) {
-    __shared__ FrameLds sf[BATCH ? NR_MAX_BATCH : 1];
-    if constexpr (BATCH) {
-        for (int i = threadIdx.x; i < T.nframes * 18; i += blockDim.x) {  // as k_trace
-            const int f = i / 18, w = i - 18 * f;
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(T.frames + f);
-            reinterpret_cast<uint32_t *>(sf + f)[w] = w < 12 ? src[w] : (w < 16 ? src[16 + w] : (w == 16 ? src[32] : 0u));
-        }
-    }
-    uint16_t *slp = reinterpret_cast<uint16_t *>(nr_smem16);
-    float *sfl = reinterpret_cast<float *>(nr_smem16 + M.x3lp_bytes);
-    for (int i = threadIdx.x; i < M.x3lp_bytes / 16; i += blockDim.x)
-        reinterpret_cast<int4 *>(slp)[i] = reinterpret_cast<const int4 *>(M.x3lp)[i];
-    for (int i = threadIdx.x; i < M.x3fl_bytes / 16; i += blockDim.x)
-        reinterpret_cast<int4 *>(sfl)[i] = reinterpret_cast<const int4 *>(M.x3fl)[i];
-    __syncthreads();
-    __shared__ float4 stash[4][STASH];
-    __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
-    const int lane = lane_id();
-    const int wid = threadIdx.x >> 6;
-    const float fr = (float)A.frame;
-    const double zoff0 = sphere_zoff(A.frame);
-    auto out_of = [&](int f) -> gptr_u32 { return (gptr_u32)(BATCH ? sf[f].out : A.out); };
-    auto zoff_of = [&](int f) -> double { return BATCH ? sf[f].zoff : zoff0; };
-    auto fr_of = [&](int f) -> float { return BATCH ? (M.in0 == 4 ? sf[f].frame_f : 0.0f) : fr; };
-    auto put = [&](int f, uint32_t i, uint32_t v) { out_of(f)[i] = v; };
-    auto dir_of = [&](int f, uint32_t pxl) -> F3 {
-        const int lr = (int)udiv_r(pxl, (uint32_t)A.W, A.inv_w);
-        return ray_dir(A, T, BATCH ? sf[f].inv_view : A.inv_view, (int)(pxl - (uint32_t)lr * A.W), lr);
-    };
-    // the slots k_trace filled (it has ended: same stream)
-    const uint32_t total = min((uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(T.ho_ctr, __ATOMIC_RELAXED,
-                                                                                               __HIP_MEMORY_SCOPE_AGENT)),
-                               T.ho_cap);
-    const int q4 = lane & 3;
-    F3 p = mk3(0, 0, 0), d = mk3(0, 0, 0);
-    float tfar = 0.0f;
-    uint32_t pix = 0;
-    int ff = 0, it = -1, maxit = 0, nstash = 0;
-    uint32_t nfine = 0, nconv = 0;
-    bool qdone = false;
-    while (true) {
-        nstash = __builtin_amdgcn_readfirstlane(nstash);
-        qdone = __builtin_amdgcn_readfirstlane((int)qdone) != 0;
-        // ---- refill: free lanes take the next hand-off slots (empty slots leave the lane free)
-        if (!qdone) {
-            const uint64_t freem = __ballot(it < 0);
-            const uint32_t nfree = (uint32_t)__popcll(freem);
-            if (nfree >= 16) {
-                uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(T.ho_ctr + 1, nfree);
-                const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-                const uint32_t got = base < total ? min(nfree, total - base) : 0u;
-                if (got < nfree) qdone = true;
-                const uint32_t rank = rank_below(freem);
-                if (it < 0 && rank < got) {
-                    const uint2 q = T.ho_q[base + rank];
-                    if (q.y != HO_EMPTY) {
-                        const float4 hp = T.ho_p[base + rank];
-                        p = mk3(hp.x, hp.y, hp.z);
-                        tfar = hp.w;
-                        pix = q.x;
-                        it = (int)(q.y & 0xffffffu);
-                        ff = BATCH ? (int)(q.y >> 24) : 0;
-                        d = dir_of(ff, pix);
-                    }
-                }
-            }
-        }
-        const uint64_t lm = __ballot(it >= 0);
-        // ---- colour stashed converged rays: 16 rays x 4 tetrahedron samples per pass (k_trace's
-        // shading pass with NX3 normals, the fp32x3 pack from LDS)
-        while (nstash >= 16 || (qdone && nstash > 0 && !lm)) {
-            const int nb = min(16, nstash);
-            const int k = lane >> 2;
-            const int e = nstash - nb + (k < nb ? k : 0);
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            const float4 sp = stash[wid][e];
-            const int sfr = BATCH ? (int)stash_f[wid][e] : 0;
-            int qo = q4;
-            asm volatile("" : "+v"(qo));
-            const F3 tp = mk3((qo == 0 || qo == 3) ? 1.0f : -1.0f, qo >= 2 ? 1.0f : -1.0f, (qo & 1) ? 1.0f : -1.0f);
-            const F3 pq = add3(mk3(sp.x, sp.y, sp.z), mul3s(tp, NORMAL_EPSILON));
-            const uint32_t smask = (1u << ((4 * nb + 15) >> 4)) - 1u;
-            const float sdf = mlp16_x3_normal<false>(M, M.pk, slp, sfl, fr_of(sfr), pq.x, pq.y, pq.z, smask);
-            const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
-            const F3 c1 = quad_bcast3_1(cq), c2 = quad_bcast3_2(cq), c3 = quad_bcast3_3(cq);
-            if (k < nb && q4 == 0 && !T.itmap) {
-                const F3 nrm = normalize3(add3(add3(add3(cq, c1), c2), c3));
-                const uint32_t pxl = __float_as_uint(sp.w);
-                const F3 rd = A.color_type == NR_COLOR_FACING ? dir_of(sfr, pxl) : mk3(0.0f, 0.0f, 0.0f);
-                const float *nmx = BATCH ? (const float *)((const __attribute__((address_space(1))) float *)T.frames[sfr].normal)
-                                         : A.normal;
-                put(sfr, pxl, shade_color(A, nmx, nrm, rd));
-            }
-            nconv += (uint32_t)nb;
-            nstash -= nb;
-        }
-        if (!lm) {
-            if (qdone && nstash == 0) break;
-            continue;
-        }
-        // ---- fp32x3 evaluation of every live point, then singleMarch's step (as k_trace's)
-        const float fsdf = mlp16_x3_normal<false>(M, M.pk, slp, sfl, fr_of(ff), p.x, p.y, p.z, tiles_of(lm));
-        nfine += (uint32_t)__popcll(lm);
-        bool conv = false;
-        if (it >= 0) {
-            const float ts = scene_sdf(p, fsdf, A.scene, zoff_of(ff));
-            tfar -= ts;
-            int used = 0;
-            if (tfar <= 0) {
-                put(ff, pix, 0u);
-                used = it + 1;
-            } else {
-                p = add3(p, mul3s(d, ts));
-                if (ts < MARCHING_EPSILON) {
-                    if (it + 1 < A.max_steps) {
-                        conv = true;
-                        used = it + 2;
-                    } else {
-                        put(ff, pix, 0u);
-                        used = it + 1;
-                    }
-                } else if (++it >= A.max_steps) {
-                    put(ff, pix, 0u);
-                    used = A.max_steps;
-                }
-            }
-            if (used) {
-                it = -1;
-                maxit = max(maxit, used);
-                if (T.itmap) put(ff, pix, (uint32_t)used);
-                if (T.bcost) {
-                    const int yy = (int)(pix / (uint32_t)A.W), xx = (int)(pix - (uint32_t)yy * A.W);
-                    atomicMax(T.bcost + (yy >> 3) * T.bw + (xx >> 3), (uint32_t)used);
-                }
-            }
-        }
-        const uint64_t cm = __ballot(conv);
-        if (conv) {
-            const int slot = nstash + (int)rank_below(cm);
-            stash[wid][slot] = make_float4(p.x, p.y, p.z, __uint_as_float(pix));
-            if constexpr (BATCH) stash_f[wid][slot] = (uint8_t)ff;
-        }
-        nstash += (int)__popcll(cm);
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) maxit = max(maxit, __shfl_xor(maxit, off));
-    if (lane == 0) {
-        // fp32x3 evaluations are ray-steps of the frame and the endgame's evaluations
-        if (nfine) {
-            atomicAdd(T.stats + 0, (unsigned long long)nfine);
-            atomicAdd(T.stats + 4, (unsigned long long)nfine);
-        }
-        if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
-        if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
-    }
-}
-
 // one k_trace instance: bf16/fp16 with fp32x3 normals when the network has the pack (M.x3n)
 template <int PREC, bool PROBE, bool STAMPS, bool BATCH>
 static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const TraceArgs &T, int grid, int sm,
@@ -1201,18 +1110,14 @@ static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const Tr
     if constexpr (LOWP && !PROBE) {
         if constexpr (!STAMPS) {
             if (M.x3n && T.eg_tau > 0.0f) {
-                // the endgame: k_trace hands the near-surface rays off, k_fine marches them on
-                if (!T.ho_p || !T.ho_q || !T.ho_ctr) return hipErrorInvalidValue;
+                // the fine queue's LDS leaves room for NR_TRACE_BPC_EG workgroups per CU: a grid of
+                // more would queue workgroups behind the resident ones
                 int dev = 0, cus = 0;
                 if (hipGetDevice(&dev) != hipSuccess ||
                     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                     return hipErrorInvalidDevice;
-                hipError_t e = hipMemsetAsync(T.ho_ctr, 0, 2 * sizeof(uint32_t), st);
-                if (e != hipSuccess) return e;
-                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(grid), dim3(256), sm, st, A, M, T);
-                if ((e = hipGetLastError()) != hipSuccess) return e;
-                const int smf = M.x3lp_bytes + M.x3fl_bytes;
-                hipLaunchKernelGGL((k_fine<BATCH>), dim3(NR_FINE_BPC * cus), dim3(256), smf, st, A, M, T);
+                const int g = std::max(1, std::min(grid, NR_TRACE_BPC_EG * cus));
+                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(g), dim3(256), sm, st, A, M, T);
                 return hipGetLastError();
             }
         }
