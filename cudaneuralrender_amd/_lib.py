@@ -46,6 +46,7 @@ class NRStats(ctypes.Structure):
         ("launches", ctypes.c_int32),
         ("ms_total", ctypes.c_float),
         ("endgame_evals", ctypes.c_uint64),
+        ("endgame_switches", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -364,6 +364,14 @@ int default_bpc(const nr_ctx *c, size_t total, int nframes) {
     return total < 2 * M ? 3 : 4;
 }
 
+// Workgroups per CU of a persistent launch: nr_set_occupancy's value or default_bpc's, at most
+// NR_TRACE_BPC_EG for the endgame's instances (eg: a bf16/fp16 launch with T.eg_tau > 0; the
+// diagnostic stamps and probe instances march without the endgame, launch_trace_k)
+int trace_bpc(const nr_ctx *c, size_t total, int nframes, bool eg) {
+    const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, total, nframes);
+    return eg ? std::min(bpc, NR_TRACE_BPC_EG) : bpc;
+}
+
 // Rays per wave of a persistent launch (nr_set_wave_rays; 0 = automatic): an fp32 launch whose
 // pixels fill at most 2x its waves' 64-ray slots marches 32 per wave -- at 64 nearly every ray
 // is dealt in the first refills and every wave runs 4 tiles per iteration (one 1024^2 frame on
@@ -896,6 +904,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
             tot.ray_steps += st.ray_steps; tot.shade_evals += st.shade_evals; tot.rays_hit += st.rays_hit;
             tot.rays_shaded += st.rays_shaded; tot.iterations = std::max(tot.iterations, st.iterations);
             tot.launches += st.launches; tot.ms_total += st.ms_total; tot.endgame_evals += st.endgame_evals;
+            tot.endgame_switches += st.endgame_switches;
         }
         memcpy(c->inv_view, iv, sizeof iv);
         memcpy(c->normal, nm, sizeof nm);
@@ -966,7 +975,7 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,
         // so the extra waves per SIMD lift the bulk rate instead of lengthening the tail)
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix * n, n);
+        const int bpc = trace_bpc(c, npix * n, n, T.eg_tau > 0.0f && c->mlp16.x3n);
         int grid = (int)std::min<size_t>((npix * n + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         T.take = wave_rays_for(c, npix * n, grid);
@@ -994,11 +1003,12 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
     if (c->profiling) c->prof_renders += nframes;
     HIPCHK(c, hipEventRecord(c->ev1, s));
     if (stats) {
-        unsigned long long hs[5];
+        unsigned long long hs[6];
         HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         st.ray_steps = hs[0];
         st.endgame_evals = hs[4];
+        st.endgame_switches = hs[5];
         st.rays_hit = hs[1];
         st.iterations = (int32_t)hs[2];
         st.rays_shaded = hs[3];
@@ -1092,7 +1102,8 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.bw = bw;
         T.nblocks = bw * bh;
         T.itmap = (c->debug & 8) != 0;
-        T.eg_tau = endgame_tau(c, max_steps);
+        // the stamps instance (nr_set_debug bit 0) marches without the endgame
+        T.eg_tau = (c->debug & 1) ? 0.0f : endgame_tau(c, max_steps);
         {
             const int sp = spread_for(c, 1, npix);
             T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;
@@ -1106,7 +1117,7 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
             T.order = c->order_valid ? c->d_order[c->order_cur] : nullptr;
             T.bcost = c->d_bcost;
         }
-        const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, npix, 1);
+        const int bpc = trace_bpc(c, npix, 1, T.eg_tau > 0.0f && c->mlp16.x3n);
         int grid = (int)std::min<size_t>((npix + 255) / 256, (size_t)cus * bpc);
         if (grid < 1) grid = 1;
         T.take = wave_rays_for(c, npix, grid);
@@ -1155,11 +1166,12 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         HIPCHK(c, hipEventRecord(c->ev1, s));
         if (loc != NR_DEVICE) HIPCHK(c, hipMemcpyAsync(out, dout, npix * 4, hipMemcpyDeviceToHost, s));
         if (stats) {
-            unsigned long long hs[5];
+            unsigned long long hs[6];
             HIPCHK(c, hipMemcpyAsync(hs, T.stats, sizeof hs, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             st.ray_steps = hs[0];
             st.endgame_evals = hs[4];
+            st.endgame_switches = hs[5];
             st.rays_hit = hs[1];
             st.iterations = (int32_t)hs[2];
             st.rays_shaded = hs[3];

@@ -44,6 +44,9 @@ struct nr_group {
     std::vector<uint32_t *> shard[2];          // per set, per rank, on its device: its shards of a call
     std::vector<size_t> shard_cap[2];          // pixels
     std::vector<hipEvent_t> sent[2];           // per set, per rank: the set's shards have been read
+                                               // (created on the device whose stream records it:
+                                               // rank r's with RCCL, the first device's with NR_GROUP_COPY)
+    std::vector<hipEvent_t> rendered[2];       // per set, per rank (on its device): its shards are written
     uint32_t *gather[2] = {nullptr, nullptr};  // first device: N x frames x shard pixels
     size_t gather_cap[2] = {0, 0};
     uint32_t *staging[2] = {nullptr, nullptr}; // first device: frames for a host destination
@@ -71,6 +74,7 @@ void release(nr_group *g) {
         for (int b = 0; b < 2; ++b) {
             if (r < (int)g->shard[b].size() && g->shard[b][r]) (void)hipFree(g->shard[b][r]);
             if (r < (int)g->sent[b].size() && g->sent[b][r]) (void)hipEventDestroy(g->sent[b][r]);
+            if (r < (int)g->rendered[b].size() && g->rendered[b][r]) (void)hipEventDestroy(g->rendered[b][r]);
         }
         if (r < (int)g->cs.size() && g->cs[r]) (void)hipStreamDestroy(g->cs[r]);
         if (r < (int)g->comm.size() && g->comm[r]) ncclCommDestroy(g->comm[r]);
@@ -119,11 +123,20 @@ int nr_group_create_ex(nr_ctx *const *ctxs, int n, int flags, nr_group **out) {
         g->shard[b].assign(n, nullptr);
         g->shard_cap[b].assign(n, 0);
         g->sent[b].assign(n, nullptr);
+        g->rendered[b].assign(n, nullptr);
     }
+    // an event is recorded on a stream of the device it was created on: rank r's transfer stream
+    // records its `sent` events with RCCL, the first device's with NR_GROUP_COPY (the peer copies
+    // all run there); the render streams only wait on them (a cross-device wait is legal)
+    const bool copy = (flags & NR_GROUP_COPY) != 0;
     for (int r = 0; r < n; ++r) {
-        if (hipSetDevice(g->dev[r]) != hipSuccess || hipStreamCreateWithFlags(&g->cs[r], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&g->sent[0][r], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->sent[1][r], hipEventDisableTiming) != hipSuccess) {
+        bool ok = hipSetDevice(g->dev[r]) == hipSuccess && hipStreamCreateWithFlags(&g->cs[r], hipStreamNonBlocking) == hipSuccess;
+        for (int b = 0; b < 2 && ok; ++b)
+            ok = hipEventCreateWithFlags(&g->rendered[b][r], hipEventDisableTiming) == hipSuccess &&
+                 hipSetDevice(copy ? g->dev[0] : g->dev[r]) == hipSuccess &&
+                 hipEventCreateWithFlags(&g->sent[b][r], hipEventDisableTiming) == hipSuccess &&
+                 hipSetDevice(g->dev[r]) == hipSuccess;
+        if (!ok) {
             release(g);
             return nr::report_error(NR_E_HIP, "nr_group_create: streams / events on device %d", g->dev[r]);
         }
@@ -189,8 +202,23 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
     if (ensure(g->dev[0], g->gather[b], g->gather_cap[b], per_rank * n) != NR_OK ||
         (loc != NR_DEVICE && ensure(g->dev[0], g->staging[b], g->staging_cap[b], (size_t)W * H * nframes) != NR_OK))
         return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "gather buffer");
+    // ---- a fault of an earlier asynchronous call (its renders or transfers) ends this one first
+    const bool async = (g->flags & NR_GROUP_ASYNC) != 0;
+    if (async)
+        for (int r = 0; r < n; ++r) {
+            hipError_t q = hipSetDevice(g->dev[r]);
+            if (q == hipSuccess) q = hipStreamQuery(g->cs[r]);
+            if (q != hipSuccess && q != hipErrorNotReady)
+                return nr::report_error(NR_E_HIP, "nr_group_render_batch: an earlier call failed on device %d: %s", g->dev[r],
+                                        hipGetErrorString(q));
+        }
     // ---- every context renders its shard of every frame, in parallel, into set b once the
-    // transfer that last read set b is done
+    // transfer that last read set b is done.  Synchronous groups (and calls that ask for the
+    // statistics, which are read from the device) wait for each render here, so that a fault
+    // surfaces before any transfer; NR_GROUP_ASYNC only enqueues it: the transfer streams wait
+    // for it device-side (`rendered`), and the host returns to submit the next call while this
+    // one renders.  Its launch errors still end the call before the gather; a fault during the
+    // march surfaces at the next call or at nr_group_synchronize.
     std::vector<int> rc(n, NR_OK);
     std::vector<nr_stats> st(n);
     std::vector<std::string> msg(n);
@@ -200,16 +228,30 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             msg[r] = "hipSetDevice failed";
             return;
         }
-        if (g->calls >= 2 && hipStreamWaitEvent((hipStream_t)nr::ctx_stream(g->ctx[r]), g->sent[b][r], 0) != hipSuccess) {
+        const hipStream_t rs = (hipStream_t)nr::ctx_stream(g->ctx[r]);
+        if (g->calls >= 2 && hipStreamWaitEvent(rs, g->sent[b][r], 0) != hipSuccess) {
             rc[r] = NR_E_HIP;
             msg[r] = "hipStreamWaitEvent failed";
             return;
         }
         std::vector<nr_frame> fr(frames, frames + nframes);
         for (int i = 0; i < nframes; ++i) fr[i].out = g->shard[b][r] + (size_t)i * shard_px;
-        rc[r] = nr_render_batch(g->ctx[r], fr.data(), nframes, W, H, band, n, r, max_steps, NR_DEVICE, &st[r]);
-        if (rc[r] == NR_OK) rc[r] = nr_synchronize(g->ctx[r]);  // a fault surfaces here, before the gather
-        if (rc[r] != NR_OK) msg[r] = nr_last_error(g->ctx[r]);
+        rc[r] = nr_render_batch(g->ctx[r], fr.data(), nframes, W, H, band, n, r, max_steps, NR_DEVICE, stats ? &st[r] : nullptr);
+        if (rc[r] == NR_OK && !async) rc[r] = nr_synchronize(g->ctx[r]);  // a fault surfaces here, before the gather
+        if (rc[r] != NR_OK) {
+            msg[r] = nr_last_error(g->ctx[r]);
+            return;
+        }
+        if (hipEventRecord(g->rendered[b][r], rs) != hipSuccess) {
+            rc[r] = NR_E_HIP;
+            msg[r] = "hipEventRecord failed";
+            return;
+        }
+        const hipError_t q = hipStreamQuery(rs);  // a fault already known on this context's stream
+        if (q != hipSuccess && q != hipErrorNotReady) {
+            rc[r] = NR_E_HIP;
+            msg[r] = hipGetErrorString(q);
+        }
     };
     if (n == 1) {
         work(0);
@@ -224,10 +266,16 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             const std::string m = "shard " + std::to_string(r) + " (device " + std::to_string(g->dev[r]) + "): " + msg[r];
             return nr::report_error(rc[r], "nr_group_render_batch: %s", m.c_str());
         }
+    // ---- the transfers of set b start once its shards are rendered (device-side waits)
+    const bool copy = (g->flags & NR_GROUP_COPY) != 0;
+    for (int r = 0; r < n; ++r)
+        if (hipSetDevice(copy ? g->dev[0] : g->dev[r]) != hipSuccess ||
+            hipStreamWaitEvent(copy ? g->cs[0] : g->cs[r], g->rendered[b][r], 0) != hipSuccess)
+            return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "transfer wait");
     ++g->calls;
     hipStream_t c0 = g->cs[0];
     // ---- one gather of every frame's shards to the first device, on the communication streams
-    if (g->flags & NR_GROUP_COPY) {
+    if (copy) {
         if (hipSetDevice(g->dev[0]) != hipSuccess)
             return nr::report_error(NR_E_HIP, "nr_group_render_batch: %s", "hipSetDevice");
         for (int r = 0; r < n; ++r)
@@ -280,6 +328,7 @@ int nr_group_render_batch(nr_group *g, const nr_frame *frames, int nframes, int 
             t.launches += st[r].launches;
             t.ms_total = std::max(t.ms_total, st[r].ms_total);
             t.endgame_evals += st[r].endgame_evals;
+            t.endgame_switches += st[r].endgame_switches;
         }
         *stats = t;
     }

@@ -3,6 +3,14 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Workgroups per CU the persistent tracer's endgame instances (bf16/fp16 with nr_set_endgame) are
+// built for: their registers (161 VGPRs) and the fine queue's LDS leave room for this many, so the
+// host caps their grid at it (nr_api.hip trace_bpc; a larger grid would queue workgroups behind the
+// resident ones)
+#ifndef NR_TRACE_BPC_EG
+#define NR_TRACE_BPC_EG 3
+#endif
+
 namespace nr {
 
 // Network packs resident in device memory, staged into LDS by every block.

@@ -16,6 +16,12 @@
 #include "nr_device.h"
 #include "nr_mlp16_asm.h"
 
+// A/B experiment builds only (make EXTRA=-DNR_MLP16_EXP=n; wrong values): 1 no final layer,
+// 2 no input range check, 4 no input-layer split in k_mlp16's stream path
+#ifndef NR_MLP16_EXP
+#define NR_MLP16_EXP 0
+#endif
+
 namespace nr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -586,6 +592,16 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
     if constexpr (NH == 7) {
         if (stream) {
             u32x4 kk[4][2];
+#if NR_MLP16_EXP & 4
+            // experiment: the input layer's split replaced by two conversions (wrong values)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const uint32_t p0 = cvt2<PREC>(x[s], y[s]), q = cvt2<PREC>(z[s], x[s]);
+                kk[2 * s][0] = (u32x4){p0, q, p0, q};
+                kk[2 * s + 1][0] = (u32x4){q, p0, q, p0};
+            }
+            if (0)
+#endif
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 // the input layer's B operands exactly as below
@@ -607,6 +623,12 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
                 for (int t = 0; t < 2; ++t) kk[2 * s + t][0] = (u32x4){w0[t], w1[t], w2[t], w3[t]};
             }
             mlp7_x4_stream<PREC, CL>(lp, fl, kk);
+#if NR_MLP16_EXP & 1
+            // experiment: no final layer (wrong values)
+            out[0] = __uint_as_float(kk[0][0][0] ^ kk[1][1][3]);
+            out[1] = __uint_as_float(kk[2][0][0] ^ kk[3][1][3]);
+            return;
+#endif
             const u32x4 *F4 = reinterpret_cast<const u32x4 *>(lp + lp32_final(7));
             const u32x4 wf[2] = {F4[h], F4[2 + h]};
             const float bf = fl[32 + 32 * 7];

@@ -204,9 +204,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // (3 workgroups per CU: the fine pass's registers -- 161 VGPRs; at 4 per CU, <= 128 VGPRs, the
 // spills cost C3 +25 %, C5 +40-55 %; a pass per 64 queued rays instead of 32: C5 batch +5-10 %;
 // profiles/r5_ab_eg.txt)
-#ifndef NR_TRACE_BPC_EG
-#define NR_TRACE_BPC_EG 3
-#endif
+// (NR_TRACE_BPC_EG: nr_kernels.h, where the host side caps the grid with it)
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false>
 __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
                                   : PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
@@ -256,6 +254,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
     __shared__ uint32_t fq_i[EG ? 4 : 1][FQ];
     int nfq = 0;        // rays in the wave's fine queue (EG)
     uint32_t nfine = 0;  // fp32x3 march evaluations (EG)
+    uint32_t nswitch = 0;  // rays handed to the fine queue (EG; wave-uniform)
     const int lane = lane_id();
     const int wid = threadIdx.x >> 6;
     const long nchunks = T.nblocks;
@@ -770,6 +769,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
                     it = -1;
                 }
                 nfq += (int)__popcll(hm);
+                nswitch += (uint32_t)__popcll(hm);
             }
         }
         if (it >= 0) {
@@ -843,6 +843,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
         if (nconv) atomicAdd(T.stats + 3, (unsigned long long)nconv);
         if (maxit) atomicMax(T.stats + 2, (unsigned long long)maxit);
         if (EG && nfine) atomicAdd(T.stats + 4, (unsigned long long)nfine);
+        if (EG && nswitch) atomicAdd(T.stats + 5, (unsigned long long)nswitch);
     }
 }
 
@@ -976,9 +977,13 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             const unsigned long long ta = __builtin_amdgcn_s_memtime();
 #endif
             constexpr float XB = LP_INPUT_BOUND, FB = LP_INPUT_BOUND;
+#if NR_MLP16_EXP & 2
+            const bool ok = true;
+#else
             const bool ok = __builtin_fabsf(x[0]) <= XB && __builtin_fabsf(y[0]) <= XB && __builtin_fabsf(z[0]) <= XB &&
                             __builtin_fabsf(f[0]) <= FB && __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB &&
                             __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
+#endif
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
                 mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
             else
@@ -1110,14 +1115,8 @@ static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const Tr
     if constexpr (LOWP && !PROBE) {
         if constexpr (!STAMPS) {
             if (M.x3n && T.eg_tau > 0.0f) {
-                // the fine queue's LDS leaves room for NR_TRACE_BPC_EG workgroups per CU: a grid of
-                // more would queue workgroups behind the resident ones
-                int dev = 0, cus = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                    return hipErrorInvalidDevice;
-                const int g = std::max(1, std::min(grid, NR_TRACE_BPC_EG * cus));
-                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(g), dim3(256), sm, st, A, M, T);
+                // the grid is at most NR_TRACE_BPC_EG workgroups per CU (nr_api.hip trace_bpc)
+                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(grid), dim3(256), sm, st, A, M, T);
                 return hipGetLastError();
             }
         }

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define NR_ABI_VERSION 2   /* 2: nr_stats.endgame_evals, nr_set_endgame (round 5) */
+#define NR_ABI_VERSION 3   /* 2: nr_stats.endgame_evals, nr_set_endgame (round 5); 3: nr_stats.endgame_switches (round 6) */
 
 /* status codes */
 #define NR_OK 0
@@ -81,6 +81,9 @@ typedef struct nr_stats {
     float ms_total;          /* device time of the render, HIP events */
     uint64_t endgame_evals;  /* bf16/fp16 with the endgame (nr_set_endgame): the march evaluations
                                 in fp32x3, included in ray_steps */
+    uint64_t endgame_switches; /* the rays handed to the endgame: each one's switch point is evaluated
+                                in 16 bits and again in fp32x3, and both evaluations are counted in
+                                ray_steps (ray_steps - endgame_switches counts every march point once) */
 } nr_stats;
 
 /* ---- context ------------------------------------------------------------ */
@@ -192,7 +195,12 @@ int nr_group_create(nr_ctx *const *ctxs, int n, nr_group **out);
  * group's communication streams, so the next call's render overlaps this call's transfer (shard
  * and gather buffers are double-buffered): frames[i].out of an NR_DEVICE call is complete after
  * nr_group_synchronize -- or, without the flag, when the call returns.  A call with host outputs
- * (loc != NR_DEVICE) always returns with its frames written. */
+ * (loc != NR_DEVICE) always returns with its frames written.  Round 6: with NR_GROUP_ASYNC and
+ * stats == NULL the renders are only enqueued too (the transfer streams wait for them device-side),
+ * so the host submits call k + 1 while call k renders; a launch error still ends the call before
+ * any transfer, a fault during the march is returned by the next call or nr_group_synchronize.
+ * Asking for stats makes the call wait for its renders (the counters are read from the devices).
+ * With NR_GROUP_COPY the contexts may sit on distinct GPUs as well. */
 #define NR_GROUP_COPY 1
 #define NR_GROUP_ASYNC 2
 int nr_group_create_ex(nr_ctx *const *ctxs, int n, int flags, nr_group **out);
@@ -239,7 +247,7 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * wave iterations, shader-clock cycles spent in refill, shading, MLP, scene, step, and within
  * refill (bf16/fp16 tracers) in the queue reservation, bulk ray generation and dealing; after
  * the queue drained: cycles in refill + shading + step, MLP, scene, iterations with at most
- * 4 rays};
+ * 4 rays}; the stamps instance marches bf16/fp16 without the endgame (the pure 16-bit march);
  * nr_debug_stamps copies the last
  * frame's (16 u64 per wave, *n = waves).  Bit 3 = iteration map: the persistent
  * schedule writes each hit pixel's iteration count instead of its colour.  Bit 6 =
@@ -276,7 +284,8 @@ int nr_set_endgame(nr_ctx *ctx, float tau);
  * only the order work is handed out changes).  on = 2: each block's cost is the max over its
  * 3x3 neighbourhood (for a moving camera, whose silhouettes shift between frames). */
 int nr_set_temporal_order(nr_ctx *ctx, int on);
-/* Persistent-schedule grid: blocks of 4 waves per CU (0 = default). */
+/* Persistent-schedule grid: blocks of 4 waves per CU (0 = default).  A bf16/fp16 launch with the
+ * endgame on runs at most 3 per CU (its instances are built for that), whatever is set here. */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
 /* Rays per wave (persistent schedule, 1-64; 0 = automatic, the default): a wave marches at
  * most this many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or

@@ -1205,8 +1205,10 @@ int or_render(int nlayers, const int *dims, const float *params,
  * here). */
 static float g_eg_tau = 0.0f;
 static long long g_eg_evals = 0;
+static long long g_eg_switches = 0;  /* rays switched (each one's switch point is evaluated twice) */
 void or_set_endgame(float tau) { g_eg_tau = tau; }
 long long or_endgame_evals(void) { return g_eg_evals; }
+long long or_endgame_switches(void) { return g_eg_switches; }
 
 int or_render_ex(int nlayers, const int *dims, const float *params,
                  const float *inv_view, const float *normal, int frame,
@@ -1246,6 +1248,7 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
     unsigned char *fine = (unsigned char *)calloc(npix, 1);
     long *redo = (long *)calloc(npix, sizeof(long));
     g_eg_evals = 0;
+    g_eg_switches = 0;
     if (!mask || !idmap || !points || !ray || !far_ || !batch || !sdf || !bprec || !fine || !redo) {
         free(mask); free(idmap); free(points); free(ray); free(far_); free(batch); free(sdf); free(bprec);
         free(fine); free(redo);
@@ -1324,6 +1327,7 @@ int or_render_ex(int nlayers, const int *dims, const float *params,
                     fine[id] = 1;
                     redo[nredo++] = id;
                 }
+            g_eg_switches += nredo;
             if (nredo) {
                 float *xb = (float *)malloc(sizeof(float) * (size_t)nredo * ni);
                 float *yb = (float *)malloc(sizeof(float) * (size_t)nredo);

@@ -67,6 +67,8 @@ def lib():
         L.or_set_endgame.argtypes = [ctypes.c_float]
         L.or_endgame_evals.restype = ctypes.c_longlong
         L.or_endgame_evals.argtypes = []
+        L.or_endgame_switches.restype = ctypes.c_longlong
+        L.or_endgame_switches.argtypes = []
         _lib = L
     return _lib
 
@@ -140,6 +142,7 @@ class OracleNet:
         st = dict(zip(keys, (int(v) for v in stats)))
         if endgame > 0:
             st["endgame_evals"] = int(lib().or_endgame_evals())
+            st["endgame_switches"] = int(lib().or_endgame_switches())
         lib().or_set_endgame(0.0)
         return out, st
 

@@ -41,6 +41,9 @@ def _check(img, st, ref, rst):
     assert np.array_equal(img, ref), int((img != ref).sum())
     assert st["ray_steps"] == rst["ray_steps"], (st, rst)
     assert st["endgame_evals"] == rst["endgame_evals"] > 0, (st, rst)
+    # the rays handed off (round 6): each one's switch point is counted twice in ray_steps
+    assert st["endgame_switches"] == rst["endgame_switches"] > 0, (st, rst)
+    assert st["endgame_switches"] <= st["endgame_evals"]
     assert st["rays_shaded"] == rst["rays_shaded"], (st, rst)
 
 
@@ -75,6 +78,7 @@ def test_endgame_default_on_and_off(chrome):
     ref_pure, rp = net.render(128, 128, iv, nm, **kw)
     assert np.array_equal(dflt, ref_eg) and sd["endgame_evals"] > 0
     assert np.array_equal(pure, ref_pure) and sp["endgame_evals"] == 0 and sp["ray_steps"] == rp["ray_steps"]
+    assert sp["endgame_switches"] == 0 and sd["endgame_switches"] > 0
     assert not np.array_equal(dflt, pure)
 
 
@@ -120,15 +124,17 @@ def test_endgame_batch_equals_single_frames(chrome, prec):
         for iv, nm, f in cams:
             r.set_view(iv, nm, f)
             singles.append(r.render(144, 128, 128))
-    tot_steps = tot_eg = 0
+    tot_steps = tot_eg = tot_sw = 0
     for (iv, nm, f), img, (one, st) in zip(cams, imgs, singles):
         ref, rst = net.render(144, 128, iv, nm, frame=f, color_type=1, matcap=chrome, max_steps=128, nthreads=16,
                               precision=PREC[prec], endgame=nr.NR_ENDGAME_DEFAULT)
         assert np.array_equal(img, ref) and np.array_equal(one, ref), (f, int((img != ref).sum()))
         assert st["ray_steps"] == rst["ray_steps"] and st["endgame_evals"] == rst["endgame_evals"]
+        assert st["endgame_switches"] == rst["endgame_switches"]
         tot_steps += rst["ray_steps"]
         tot_eg += rst["endgame_evals"]
-    assert bst["ray_steps"] == tot_steps and bst["endgame_evals"] == tot_eg
+        tot_sw += rst["endgame_switches"]
+    assert bst["ray_steps"] == tot_steps and bst["endgame_evals"] == tot_eg and bst["endgame_switches"] == tot_sw
 
 
 def test_endgame_four_input_network_frame_bound():

@@ -27,11 +27,12 @@ def test_library_exports_every_header_symbol():
     missing = [s for s in syms if not hasattr(L, s)]
     assert not missing, missing
     assert sorted(_lib.EXPORTS) == syms, "Python binding out of sync with the header"
-    assert L.nr_abi_version() == 2
+    assert L.nr_abi_version() == 3
     # the ctypes mirror of nr_stats and the header's default endgame threshold
     txt = open(os.path.join(REPO, "include", "neural_render.h")).read()
     assert float(re.search(r"#define NR_ENDGAME_DEFAULT ([0-9.]+)f", txt).group(1)) == nr.NR_ENDGAME_DEFAULT
-    assert ctypes.sizeof(_lib.NRStats) == 56 and _lib.NRStats.endgame_evals.offset == 48
+    assert ctypes.sizeof(_lib.NRStats) == 64 and _lib.NRStats.endgame_evals.offset == 48
+    assert _lib.NRStats.endgame_switches.offset == 56
 
 
 def test_create_without_gpu_fails_cleanly():
