@@ -241,6 +241,11 @@ typedef struct nr_kernel_prof {
 } nr_kernel_prof;
 int nr_set_profiling(nr_ctx *ctx, int on);
 int nr_prof_collect(nr_ctx *ctx, nr_kernel_prof *out);
+/* The pixel contract per schedule (round 6): fp32 frames are identical on all three schedules.
+ * bf16 / fp16 frames depend on the schedule: the persistent schedule (the default) applies the
+ * endgame (nr_set_endgame), the wavefront schedule marches in pure 16 bits -- its frames equal
+ * the persistent schedule's with nr_set_endgame(ctx, 0) -- and the layered schedule renders fp32
+ * whatever the precision.  tests/test_gpu_endgame.py test_schedule_pixel_contract asserts this. */
 int nr_set_schedule(nr_ctx *ctx, int schedule);
 /* Diagnostics: flags bit 0 = per-wave s_memrealtime stamps in k_trace
  * {start, pixel queue drained, end (100 MHz), (wave iterations after the drain << 32) |

@@ -179,3 +179,29 @@ def test_endgame_rejects_bad_threshold():
         for bad in (-1.0, float("nan"), float("inf")):
             with pytest.raises(nr.NRError):
                 r.set_endgame(bad)
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_schedule_pixel_contract(chrome, prec):
+    """The documented per-schedule rule for 16-bit frames at default settings (neural_render.h,
+    nr_set_schedule): persistent = the endgame frame, wavefront = the persistent frame with
+    nr_set_endgame(0) (the pure 16-bit march), layered = the fp32 frame; each against the oracle."""
+    net = _oracle("plane_1")
+    iv, nm = nr.camera(-12.0, 35.0, 2.1)
+    kw = dict(color_type=1, matcap=chrome, max_steps=128, nthreads=16)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("plane_1")).set_precision(prec)
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        pers, _ = r.render(128, 120, 128)
+        r.set_schedule("wavefront")
+        wave, _ = r.render(128, 120, 128)
+        r.set_schedule("layered")
+        lay, _ = r.render(128, 120, 128)
+        r.set_schedule("persistent").set_endgame(0)
+        pure, _ = r.render(128, 120, 128)
+    ref_eg, _ = net.render(128, 120, iv, nm, precision=PREC[prec], endgame=nr.NR_ENDGAME_DEFAULT, **kw)
+    ref_pure, _ = net.render(128, 120, iv, nm, precision=PREC[prec], **kw)
+    ref_f32, _ = net.render(128, 120, iv, nm, precision=0, **kw)
+    assert np.array_equal(pers, ref_eg)
+    assert np.array_equal(wave, pure) and np.array_equal(wave, ref_pure)
+    assert np.array_equal(lay, ref_f32)
