@@ -47,6 +47,10 @@ struct nr_ctx {
     bool fp32_normals = false;   // nr_set_debug bit 15: the bf16/fp16 tracers' normals in fp32 (A/B)
     float eg_tau = NR_ENDGAME_DEFAULT;  // nr_set_endgame: bf16/fp16 persistent renders' fp32x3 endgame
     float *d_lpf16 = nullptr;
+    uint16_t *d_lps16 = nullptr;  // the 16x16x32 layout of d_lp16 / d_lpf16 (k_mlp16, 7 hidden layers)
+    float *d_lpfs16 = nullptr;
+    bool no_s16 = true;           // nr_set_debug bit 12 clear: k_mlp16 on the 32x32x16 stream (the
+                                  // default; the 16x16x32 one measured 3-5 % slower, round 6)
     MlpArgs mlp16{};  // 16-point-tile packs: k_trace, k_mlp16, k_march16, k_shade16
     bool clamp_ok = false;  // the bf16 pack is scaled for the clamped ReLU (pack_lowp_32)
     bool no_stream = false;  // nr_set_debug bit 11: the 16-bit MLP's builtin form (MlpArgs::lp_stream)
@@ -172,6 +176,7 @@ int free_network(nr_ctx *c) {
     for (auto *p : c->d_b) (void)hipFree(p);
     c->d_W.clear(); c->d_b.clear();
     dfree(c->d_pack16); dfree(c->d_lp16); dfree(c->d_lpf16); dfree(c->d_x3lp); dfree(c->d_x3fl);
+    dfree(c->d_lps16); dfree(c->d_lpfs16);
     c->fused = false;
     if (c->lgraph) { (void)hipGraphExecDestroy(c->lgraph); c->lgraph = nullptr; }
     c->lkey.clear();
@@ -200,6 +205,8 @@ int upload_lowp(nr_ctx *c) {
     c->mlp16.lp_clamp = 0;
     dfree(c->d_x3lp); dfree(c->d_x3fl);
     c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
+    dfree(c->d_lps16); dfree(c->d_lpfs16);
+    c->mlp16.lps = nullptr; c->mlp16.lpfs = nullptr;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
     std::vector<uint16_t> a;
     std::vector<float> f;
@@ -219,6 +226,18 @@ int upload_lowp(nr_ctx *c) {
     c->mlp16.lp_clamp = c->clamp_ok && !c->no_clamp;
     int rc = upload_pack(c, a, f, c->d_lp16, c->d_lpf16, c->mlp16);
     if (rc != NR_OK) return rc;
+    // k_mlp16's 16x16x32 layout of the same pack (the networks its streams take: 7 hidden layers)
+    if (c->mlp16.nh == 7) {
+        std::vector<uint16_t> sa;
+        std::vector<float> sf;
+        pack_lowp_s16(a, f, c->mlp16.nh, sa, sf);
+        MlpArgs S{};
+        if ((rc = upload_pack(c, sa, sf, c->d_lps16, c->d_lpfs16, S)) != NR_OK) return rc;
+        if (S.lp_bytes != c->mlp16.lp_bytes || S.lpf_bytes != c->mlp16.lpf_bytes)
+            return set_err(c, NR_E_INVALID, "16x16x32 pack size mismatch");
+        c->mlp16.lps = c->no_s16 ? nullptr : c->d_lps16;
+        c->mlp16.lpfs = c->no_s16 ? nullptr : c->d_lpfs16;
+    }
     // the fp32x3 pack beside it, for the normals (read from global memory); a network whose
     // pack is not valid keeps the fp32 normals
     std::vector<uint16_t> xa;
@@ -1431,6 +1450,9 @@ int nr_set_debug(nr_ctx *c, int flags) {
     c->debug = flags;
     c->no_clamp = (flags >> 9) & 1;
     c->no_stream = (flags >> 11) & 1;
+    c->no_s16 = !((flags >> 12) & 1);
+    c->mlp16.lps = c->no_s16 ? nullptr : c->d_lps16;
+    c->mlp16.lpfs = c->no_s16 ? nullptr : c->d_lpfs16;
     c->fp32_normals = (flags >> 15) & 1;
     c->mlp16.x3n = !c->fp32_normals && c->mlp16.x3lp != nullptr;
     c->mlp16.lp_stream = !c->no_stream;

@@ -97,6 +97,13 @@ bool pack_fp32_16(const std::vector<int> &dims, const std::vector<std::vector<fl
 bool pack_lowp_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,
                   const std::vector<std::vector<float>> &biases, int precision,
                   std::vector<uint16_t> &a_ops, std::vector<float> &bias, int *clamp = nullptr);
+// The 16x16x32 form of pack_lowp_32's output for k_mlp16 (round 6; nr_mlp16_asm.h NR_S16_*,
+// tools/gen_mlp_asm.py build_s16): the same elements re-ordered -- the input layer's rows permuted,
+// each hidden layer's A operand as [half 2][lane 64][8] (lane (row j, group g): output unit
+// U(half, j), k-slot 8g + e: input unit V(g, e)) and its bias as [group 4][half 2][4]; the final
+// layer unchanged.  Same sizes as the 32x32x16 pack.
+void pack_lowp_s16(const std::vector<uint16_t> &a32, const std::vector<float> &f32, int nh,
+                   std::vector<uint16_t> &a16, std::vector<float> &f16);
 // ok (if not null) = 1 when the scales exist (every scaled weight and bound inside fp16's range);
 // otherwise the kernels run the fp32 MLP for every point
 bool pack_x3_32(const std::vector<int> &dims, const std::vector<std::vector<float>> &kernels,

@@ -30,6 +30,10 @@ struct MlpArgs {
     const float *x3fl;
     int x3n;                // bf16/fp16: 1 = the normals (4 MLP evaluations per coloured ray) in fp32x3
                             // (mlp16_x3_normal), 0 = in fp32
+    const uint16_t *lps;    // bf16/fp16, 7 hidden layers: the 16x16x32 layout of lp / lpf for k_mlp16
+    const float *lpfs;      // (nr_pack.cpp pack_lowp_s16; null: not built, or nr_set_debug bit 12 clear)
+    int lp_s16;             // k_mlp16 only (launch_mlp16): lp / lpf ARE the 16x16x32 layout, every
+                            // chunk takes the NR_S16_* stream
 };
 
 // Per-render constants (the reference's __constant__ state, volumeRender_kernel.cu:31-35,

@@ -581,11 +581,40 @@ __device__ __forceinline__ void mlp7_x4_stream(const uint16_t *__restrict__ lp, 
 #undef NR_STREAM_OPERANDS
 }
 
+// The same with the hidden layers on v_mfma_f32_16x16x32 (round 6; k_mlp16 with MlpArgs::lp_s16,
+// the pack of nr_pack.cpp pack_lowp_s16; tools/gen_mlp_asm.py build_s16): the input layer's
+// 32x32x16 outputs are dealt to eight 16-point tiles by v_permlane16_swap and the last hidden
+// layer's back to the four 32-point tiles' final-layer operands -- the same interface and the
+// same values, bit for bit (a 16x16x32 MFMA sums its K = 32 as two chained K = 16 steps of the
+// 8-product blocks, profiles/r5_mfma_peak_random.txt (4), and the pack keeps each block's units).
+// Registers v0-v127 (16 fewer than the 32x32x16 stream: a 16-point tile's bias is 4 registers).
+template <int PREC, bool CL>
+__device__ __forceinline__ void mlp7_x4_stream_s16(const uint16_t *__restrict__ lp, const float *__restrict__ fl,
+                                                   u32x4 (&k)[4][2]) {
+    typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+    const int lane = lane_id();
+    const uint32_t va = lds_addr(lp) + 16u * (uint32_t)lane, vb0 = lds_addr(fl) + 64u * (uint32_t)(lane >> 5),
+                   vb = lds_addr(fl) + 32u * (uint32_t)(lane >> 4);
+    f32x16 c0, c1, c2, c3;
+    u32x8 ab0, ab1, bb0, bb1;
+#define NR_S16_OPERANDS                                                                                             \
+    : "+{v[64:67]}"(k[0][0]), "=&{v[68:71]}"(k[0][1]), "+{v[72:75]}"(k[1][0]), "=&{v[76:79]}"(k[1][1]),            \
+      "+{v[80:83]}"(k[2][0]), "=&{v[84:87]}"(k[2][1]), "+{v[88:91]}"(k[3][0]), "=&{v[92:95]}"(k[3][1]),            \
+      "=&{v[0:15]}"(c0), "=&{v[16:31]}"(c1), "=&{v[32:47]}"(c2), "=&{v[48:63]}"(c3), "=&{v[96:103]}"(ab0),         \
+      "=&{v[104:111]}"(ab1), "=&{v[112:119]}"(bb0), "=&{v[120:127]}"(bb1)                                          \
+    : [va] "v"(va), [vb0] "v"(vb0), [vb] "v"(vb)                                                                   \
+    : "memory"
+    if constexpr (PREC == NR_PRECISION_BF16 && CL) asm volatile(NR_S16_BF16_CLAMP NR_S16_OPERANDS);
+    else if constexpr (PREC == NR_PRECISION_BF16) asm volatile(NR_S16_BF16_MAX NR_S16_OPERANDS);
+    else asm volatile(NR_S16_F16_MAX NR_S16_OPERANDS);
+#undef NR_S16_OPERANDS
+}
+
 template <int PREC, int NH, bool CL>
 __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh_rt, const float (&fr)[2], const float (&x)[2],
                                                const float (&y)[2], const float (&z)[2], float (&out)[2],
-                                               bool stream = false) {
+                                               bool stream = false, bool s16 = false) {
     typedef typename Lowp<PREC>::v8 v8;
     const int nh = NH > 0 ? NH : nh_rt;
     const int lane = lane_id(), h = lane >> 5;
@@ -622,7 +651,8 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
 #pragma unroll
                 for (int t = 0; t < 2; ++t) kk[2 * s + t][0] = (u32x4){w0[t], w1[t], w2[t], w3[t]};
             }
-            mlp7_x4_stream<PREC, CL>(lp, fl, kk);
+            if (s16) mlp7_x4_stream_s16<PREC, CL>(lp, fl, kk);
+            else mlp7_x4_stream<PREC, CL>(lp, fl, kk);
 #if NR_MLP16_EXP & 1
             // experiment: no final layer (wrong values)
             out[0] = __uint_as_float(kk[0][0][0] ^ kk[1][1][3]);
@@ -706,8 +736,8 @@ __device__ __forceinline__ void mlp32_lowp_128(const uint16_t *__restrict__ lp, 
 template <int PREC, bool CL>
 __device__ __forceinline__ void mlp128_lowp_cl(const uint16_t *__restrict__ lp, const float *__restrict__ fl, int in0,
                                                int nh, const float (&fr)[2], const float (&x)[2], const float (&y)[2],
-                                               const float (&z)[2], float (&out)[2], bool stream) {
-    if (nh == 7) mlp32_lowp_128<PREC, 7, CL>(lp, fl, in0, nh, fr, x, y, z, out, stream);
+                                               const float (&z)[2], float (&out)[2], bool stream, bool s16 = false) {
+    if (nh == 7) mlp32_lowp_128<PREC, 7, CL>(lp, fl, in0, nh, fr, x, y, z, out, stream, s16);
     else mlp32_lowp_128<PREC, 0, CL>(lp, fl, in0, nh, fr, x, y, z, out);
 }
 

@@ -877,7 +877,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_of(const void *p, uint3
 }
 // IN0: the network's inputs (3, or 4 with the frame): a template parameter, so that the load is
 // not behind a branch (whose join waited for it).  4-wave workgroups deal the chunks grid-stride.
-template <int PREC, int IN0>
+// S16 (bf16 / fp16, MlpArgs::lp_s16): every chunk on the 16x16x32 stream -- a separate instance,
+// so that the 32x32x16 stream's pinned registers do not share its register allocation.
+template <int PREC, int IN0, bool S16 = false>
 __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                                   : PREC == NR_PRECISION_FP32 ? NR_MLP16_WPS : NR_MLP16_WPS_LP) void k_mlp16(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y, int n) {
     constexpr int WPG = 4;  // waves per workgroup
@@ -916,7 +918,7 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                              __builtin_fabsf(f[0]) <= FB;
             const bool ok1 = __builtin_fabsf(x[1]) <= XB && __builtin_fabsf(y[1]) <= XB && __builtin_fabsf(z[1]) <= XB &&
                              __builtin_fabsf(f[1]) <= FB;
-            if (rem <= 64) {
+            if (rem <= 64 && !S16) {  // (the 16x16x32 pack serves only the 128-point stream)
                 const uint32_t tmask = rem >= 64 ? 0xfu : (1u << ((rem + 15) >> 4)) - 1u;
                 store((uint32_t)(base + lane), mlp16(M, S.s32, S.slp, S.sfl, PREC, f[0], x[0], y[0], z[0], tmask,
                                                      M.lp_clamp && __ballot(!ok0) == 0));
@@ -924,9 +926,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
             }
             float v[2];
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!(ok0 && ok1)) == 0)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, S16 || M.lp_stream != 0, S16);
             else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, v, S16 || M.lp_stream != 0, S16);
             store((uint32_t)(base + lane), v[0]);
             store((uint32_t)(base + 64 + lane), v[1]);
         };
@@ -985,9 +987,9 @@ __global__ __launch_bounds__(256, PREC == NR_PRECISION_FP32X3 ? NR_MLP16_WPS_X3
                             __builtin_fabsf(z[1]) <= XB && __builtin_fabsf(f[1]) <= FB;
 #endif
             if (PREC == NR_PRECISION_BF16 && M.lp_clamp && __ballot(!ok) == 0)
-                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, true>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, S16 || M.lp_stream != 0, S16);
             else
-                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, M.lp_stream != 0);
+                mlp128_lowp_cl<PREC, false>(S.slp, S.sfl, in0, M.nh, f, x, y, z, pv, S16 || M.lp_stream != 0, S16);
 #if NR_MLP16_STAMPS
             st_mlp += __builtin_amdgcn_s_memtime() - ta;
             ++st_n;
@@ -1083,9 +1085,17 @@ hipError_t launch_order(const uint32_t *bcost, uint32_t *order, int nblocks, int
     return hipGetLastError();
 }
 
-hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
-    const int sm = smem16_bytes(M, prec, false);
+hipError_t launch_mlp16(const MlpArgs &M0, int prec, const float *X, float *Y, long n, int grid, hipStream_t st) {
     const bool lowp = prec == NR_PRECISION_BF16 || prec == NR_PRECISION_FP16;
+    // bf16 / fp16 networks with 7 hidden layers: the 16x16x32 pack and stream (MlpArgs::lps)
+    MlpArgs M = M0;
+    M.lp_s16 = 0;
+    if (lowp && M.lps && M.lp_stream && M.nh == 7) {
+        M.lp = M.lps;
+        M.lpf = M.lpfs;
+        M.lp_s16 = 1;
+    }
+    const int sm = smem16_bytes(M, prec, false);
     // segments of at most 2^26 points: the kernel's buffer offsets (n * in0 * 4 bytes) are 32-bit
     constexpr long SEG = 1l << 26;
     for (long p0 = 0; p0 < n; p0 += SEG) {
@@ -1097,7 +1107,11 @@ hipError_t launch_mlp16(const MlpArgs &M, int prec, const float *X, float *Y, lo
         const int g = (int)std::max<long>(1, std::min<long>(grid, ((long)m + per_wg - 1) / per_wg));
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g), dim3(256), sm, st, M, x, y, m); };
         const bool four = M.in0 == 4;
-        if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
+        if (M.lp_s16 && prec == NR_PRECISION_BF16)
+            four ? go(k_mlp16<NR_PRECISION_BF16, 4, true>) : go(k_mlp16<NR_PRECISION_BF16, 3, true>);
+        else if (M.lp_s16 && prec == NR_PRECISION_FP16)
+            four ? go(k_mlp16<NR_PRECISION_FP16, 4, true>) : go(k_mlp16<NR_PRECISION_FP16, 3, true>);
+        else if (prec == NR_PRECISION_BF16) four ? go(k_mlp16<NR_PRECISION_BF16, 4>) : go(k_mlp16<NR_PRECISION_BF16, 3>);
         else if (prec == NR_PRECISION_FP16) four ? go(k_mlp16<NR_PRECISION_FP16, 4>) : go(k_mlp16<NR_PRECISION_FP16, 3>);
         else if (prec == NR_PRECISION_FP32X3) four ? go(k_mlp16<NR_PRECISION_FP32X3, 4>) : go(k_mlp16<NR_PRECISION_FP32X3, 3>);
         else four ? go(k_mlp16<NR_PRECISION_FP32, 4>) : go(k_mlp16<NR_PRECISION_FP32, 3>);

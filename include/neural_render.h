@@ -267,6 +267,9 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * frame instead of interleaving the frames in 64-pixel chunks (pixels are unaffected).  Bit 11 = the
  * bf16/fp16 MLP of 7-hidden-layer networks in its builtin-compiled form instead of the
  * software-pipelined instruction streams (nr_mlp16_asm.h; the same values, for A/B and parity).
+ * Bit 12 = nr_mlp_forward's bf16/fp16 MLP (k_mlp16, 7 hidden layers) with the hidden layers on
+ * v_mfma_f32_16x16x32 instead of 32x32x16 (round 6; the same values; 3-5 % slower for bf16 and
+ * 4-12 % for fp16, profiles/r6_mlp_s16_ab.txt, so it is an A/B form, not the default).
  * Bit 15 = the bf16/fp16 tracers' normals (the four tetrahedron
  * samples of every coloured ray) by the fp32 MLP instead of the fp32x3 split (A/B; the frames'
  * march is the same, their shading moves by the two forms' rounding). */

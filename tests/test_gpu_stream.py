@@ -2,7 +2,10 @@
 hazard-checked by tools/gen_mlp_asm.py) issue the same instructions on the same operands as the
 builtin-compiled form, in a different order: every value must be identical, bit for bit, to the
 builtin form (nr_set_debug bit 11) -- for bf16 with the clamped ReLU and with v_pk_max_i16
-(bit 9), fp16, 3- and 4-input networks, ragged sizes and inputs beyond the clamp bound."""
+(bit 9), fp16, 3- and 4-input networks, ragged sizes and inputs beyond the clamp bound.
+Round 6: nr_set_debug bit 12 runs nr_mlp_forward's hidden layers on v_mfma_f32_16x16x32 (the
+NR_S16_* streams on nr_pack.cpp's pack_lowp_s16 layout; measured slower than the default 32x32x16
+stream, kept as the A/B form); both must equal the builtin form and the oracle's restatement."""
 import numpy as np
 import pytest
 
@@ -13,6 +16,7 @@ pytestmark = pytest.mark.gpu
 PURE_16BIT = True  # the pure 16-bit march (conftest.py pure_16bit)
 NO_CLAMP = 1 << 9
 NO_STREAM = 1 << 11
+S16 = 1 << 12
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +37,8 @@ def stream_and_builtin(rend, fn, debug=0):
     return a, b
 
 
-@pytest.mark.parametrize("prec,debug", [("bf16", 0), ("bf16", NO_CLAMP), ("fp16", 0)])
+@pytest.mark.parametrize("prec,debug", [("bf16", 0), ("bf16", NO_CLAMP), ("fp16", 0), ("bf16", S16),
+                                        ("bf16", S16 | NO_CLAMP), ("fp16", S16)])
 @pytest.mark.parametrize("geom", GEOMS)
 def test_mlp_stream_equals_builtin(rend, nets, geom, prec, debug):
     dims, K, B = nets[geom]
@@ -70,13 +75,32 @@ def test_mlp_stream_four_inputs(rend, prec):
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
-def test_mlp_stream_ragged(rend, nets, prec):
+@pytest.mark.parametrize("debug", [0, S16])
+def test_mlp_stream_ragged(rend, nets, prec, debug):
     dims, K, B = nets["plane_1"]
     rend.load_mlp(dims, K, B).set_precision(prec)
     X = np.random.default_rng(23).uniform(-1.2, 1.2, size=(4096, 3)).astype(np.float32)
     try:
         for n in (1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1000, 4096):
-            a, b = stream_and_builtin(rend, lambda: rend.mlp_forward(X[:n]))
+            a, b = stream_and_builtin(rend, lambda: rend.mlp_forward(X[:n]), debug)
             assert np.array_equal(a, b), n
     finally:
         rend.set_precision("fp32")
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("debug", [0, S16])
+@pytest.mark.parametrize("geom", GEOMS)
+def test_mlp_forward_equals_oracle_restatement(rend, nets, geom, prec, debug):
+    """nr_mlp_forward (k_mlp16: the 32x32x16 stream by default, the 16x16x32 one with bit 12)
+    against the oracle's restatement of the GPU's 16-bit arithmetic (precision 1 / 2), bit for bit."""
+    import oracle
+    dims, K, B = nets[geom]
+    rend.load_mlp(dims, K, B).set_precision(prec).set_debug(debug)
+    X = np.random.default_rng(24).uniform(-1.2, 1.2, size=(16384 + 45, 3)).astype(np.float32)
+    try:
+        y = rend.mlp_forward(X)
+    finally:
+        rend.set_debug(0).set_precision("fp32")
+    ref = oracle.OracleNet(K, B).forward(X, precision=1 if prec == "bf16" else 2, nthreads=16)
+    assert np.array_equal(y, ref), int((y != ref).sum())

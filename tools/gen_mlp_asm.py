@@ -60,6 +60,10 @@ MFMA_VALU_RAW = 13
 VALU_MFMA_RAW = 3
 SRCC_WAR = 16
 SRCAB_WAR = 8
+# v_permlane16/32_swap reading a register a VALU instruction wrote (LLVM's gfx950 hazard rule
+# "VALU write vdst -> v_permlane read", cdna_hip_programming.md T21): 2 wait states.  Otherwise a
+# swap is a VALU instruction that reads and writes both of its registers.
+PERM_RAW = 2
 
 
 class Stream:
@@ -90,8 +94,10 @@ class Stream:
                 for role, r in rd:
                     if r in writes:
                         need = max(need, (SRCC_WAR if role == "C" else SRCAB_WAR) - dist)
-            elif k == "valu" and kind == "mfma" and any(r in wr for r in regs):
+            elif k in ("valu", "perm") and kind == "mfma" and any(r in wr for r in regs):
                 need = max(need, VALU_MFMA_RAW - dist)
+            elif k in ("valu", "perm") and kind == "perm" and any(r in wr for r in regs):
+                need = max(need, PERM_RAW - dist)
             dist += states
         self.nop(need)
 
@@ -196,6 +202,143 @@ def build(prec, clamp, nt=4):
     return st
 
 
+def build_s16(prec, clamp):
+    """k_mlp16's 128-point MLP with the hidden layers on v_mfma_f32_16x16x32 (round 6, VERDICT r5
+    item 1): the input layer as in build() (four 32-point tiles, v_mfma_f32_32x32x16), its outputs
+    re-dealt to eight 16-point tiles by one v_permlane16_swap per word pair, the 7 hidden layers as
+    two 16x16x32 MFMAs (output rows 0-15 and 16-31) per 16-point tile, and the last hidden layer's
+    outputs re-dealt to the 32-point tiles' B operands by the same swaps, where the final layer (the
+    caller's v_dot2c chains) reads them as it reads build()'s.
+
+    Same values as build(), bit for bit: a 16x16x32 MFMA sums its K = 32 as two chained K = 16
+    steps of the matrix core's 8-product blocks (profiles/r5_mfma_peak_random.txt (4)), and the
+    pack (nr_pack.cpp pack_lowp_s16) orders the hidden units so that lane group g of a B operand
+    holds the block the 32x32x16 form sums g-th; the input layer's rows are permuted so that the
+    swap lands each block in its group, the last hidden layer's so that the swap back gives the
+    32x32x16 form's final-layer operands.  Lane (j, g) of 16-point tile t: point 16t + j, block g.
+
+    Registers: accumulators v0-v63 (16-point tile t: v[8t:8t+3] rows 0-15, v[8t+4:8t+7] rows
+    16-31; 32-point tile T: v[16T:16T+15]), B operands v64-v95 (16-point tile t: v[64+4t:+3]; in:
+    the input layer's B operand of 32-point tile T at v[64+8T:+3]; out: 32-point tile T's final
+    operands, k-step s at v[64+8T+4s:+3] -- build()'s interface), A operands v96-v111 and biases
+    v112-v127 (two buffers each); the input layer's bias is read into v48-v63, the accumulator of
+    32-point tile 3, whose MFMA then accumulates in place.  %[va] = LDS byte address of the A
+    operands + 16 lane, %[vb0] = of the biases + 64 (lane >> 5) (the input layer's 32-point
+    layout), %[vb] = + 32 (lane >> 4) (the hidden layers': [group 4][half 2][4] per layer)."""
+    dt = "bf16" if prec == "bf16" else "f16"
+    st = Stream(8)
+    ACC = lambda t, h: 8 * t + 4 * h
+    ACC32 = lambda T: 16 * T
+    KOP = lambda t: 64 + 4 * t
+    AOP = lambda b, h: 96 + 8 * b + 4 * h
+    BIAS = lambda b, h: 112 + 8 * b + 4 * h
+    L0B = 48
+
+    def cvt(dst, src):
+        st.pad("valu", [src, src + 1], [dst])
+        if prec == "bf16" and clamp:
+            st.add(f"v_cvt_pk_bf16_f32 v{dst}, v{src}, v{src + 1} clamp", "valu", reads=[src, src + 1], writes=[dst])
+        else:
+            c = "v_cvt_pk_bf16_f32" if prec == "bf16" else "v_cvt_pk_f16_f32"
+            st.add(f"{c} v{dst}, v{src}, v{src + 1}", "valu", reads=[src, src + 1], writes=[dst])
+            st.add(f"v_pk_max_i16 v{dst}, v{dst}, 0", "valu", reads=[dst], writes=[dst])
+
+    def mfma32(T):
+        d, a, b, c = ACC32(T), AOP(0, 0), KOP(2 * T), L0B
+        reads = [("A", r) for r in rng(a, 4)] + [("B", r) for r in rng(b, 4)] + [("C", r) for r in rng(c, 16)]
+        st.pad("mfma", reads, list(rng(d, 16)))
+        st.add(f"v_mfma_f32_32x32x16_{dt} v[{d}:{d + 15}], v[{a}:{a + 3}], v[{b}:{b + 3}], v[{c}:{c + 15}]", "mfma",
+               reads=reads, writes=list(rng(d, 16)))
+
+    def mfma16(buf, t, h):
+        d, a, b, c = ACC(t, h), AOP(buf, h), KOP(t), BIAS(buf, h)
+        reads = [("A", r) for r in rng(a, 4)] + [("B", r) for r in rng(b, 4)] + [("C", r) for r in rng(c, 4)]
+        st.pad("mfma", reads, list(rng(d, 4)))
+        st.add(f"v_mfma_f32_16x16x32_{dt} v[{d}:{d + 3}], v[{a}:{a + 3}], v[{b}:{b + 3}], v[{c}:{c + 3}]", "mfma",
+               reads=reads, writes=list(rng(d, 4)))
+
+    def conv32(T, s):   # input layer, 32-point tile T, registers 8s..8s+7 -> 16-point tile 2T + s's slots
+        for q in range(4):
+            cvt(KOP(2 * T + s) + q, ACC32(T) + 8 * s + 2 * q)
+
+    def conv16(t, h):   # half h of 16-point tile t's accumulators -> B-operand words 2h, 2h + 1
+        for q in range(2):
+            cvt(KOP(t) + 2 * h + q, ACC(t, h) + 2 * q)
+
+    def swap(T, q):     # word q of 16-point tiles 2T, 2T + 1 <-> 32-point tile T's k-steps 0, 1
+        a, b = KOP(2 * T) + q, KOP(2 * T + 1) + q
+        st.pad("perm", [a, b], [a, b])
+        st.add(f"v_permlane16_swap_b32 v{a}, v{b}", "perm", reads=[a, b], writes=[a, b])
+
+    def load(dst, addr, off):
+        st.pad("lds", (), list(rng(dst, 4)))
+        st.add(f"ds_read_b128 v[{dst}:{dst + 3}], %[{addr}]" + (f" offset:{off}" if off else ""), "lds",
+               writes=list(rng(dst, 4)))
+
+    def a_loads(buf, j):
+        load(AOP(buf, 0), "va", 1024 + 2048 * j)
+        load(AOP(buf, 1), "va", 2048 + 2048 * j)
+
+    def b_loads(buf, j):
+        load(BIAS(buf, 0), "vb", 128 + 128 * j)
+        load(BIAS(buf, 1), "vb", 128 + 128 * j + 16)
+
+    wait = lambda: st.add("s_waitcnt lgkmcnt(0)", "wait")
+    # ---- input layer (32-point tiles); hidden layer 0's operands (buffer 1) load beside it
+    load(AOP(0, 0), "va", 0)
+    for i in range(4):
+        load(L0B + 4 * i, "vb0", 16 * i)
+    wait()
+    mfma32(0)
+    a_loads(1, 0)
+    mfma32(1)
+    b_loads(1, 0)
+    mfma32(2)
+    mfma32(3)
+    conv32(0, 0)
+    conv32(0, 1)
+    for q in range(4):
+        swap(0, q)
+    # ---- hidden layers l = 1..NH (j = l - 1, buffer l % 2), the conversions two 16-point tiles
+    # ahead; in layer 1 the input layer's 32-point tiles 1-3 are converted and swapped instead
+    for l in range(1, NH + 1):
+        buf, j, nxt = l % 2, l - 1, l < NH
+        wait()
+        for t in range(8):
+            for h in range(2):
+                mfma16(buf, t, h)
+                if l == 1 and t < 6:
+                    T = t // 2 + 1
+                    if t % 2 == 0:
+                        conv32(T, h)
+                    else:
+                        swap(T, 2 * h)
+                        swap(T, 2 * h + 1)
+                else:
+                    conv16((t + 2) % 8, h)
+                if nxt and (t, h) == (2, 0):
+                    a_loads(1 - buf, j + 1)
+                elif nxt and (t, h) == (3, 0):
+                    b_loads(1 - buf, j + 1)
+    # ---- the last hidden layer's outputs: tiles 2-7 converted, every pair swapped back
+    for q in range(4):
+        swap(0, q)
+    for T in range(1, 4):
+        for s in range(2):
+            conv16(2 * T + s, 0)
+            conv16(2 * T + s, 1)
+        for q in range(4):
+            swap(T, q)
+    dist, need = 0, 0
+    for text, k, rd, wr, states in reversed(st.ins):
+        if k == "mfma":
+            need = max(need, MFMA_VALU_RAW - dist, max(SRCC_WAR if role == "C" else SRCAB_WAR for role, _ in rd) - dist)
+        dist += states
+    st.nop(need)
+    check(st, inputs=[r for T in range(4) for r in rng(KOP(2 * T), 4)])
+    return st
+
+
 def check(st, inputs=None):
     """Verifies every hazard of the stream (raises on the first violation).  inputs: the registers
     the compiler's VALU wrote just before the stream (default: the k-step-0 B operands)."""
@@ -224,8 +367,10 @@ def check(st, inputs=None):
                 dist = pos[i] - (pos[wi] + st.ins[wi][4]) if wi >= 0 else pos[i]   # states in between
                 if wk == "mfma" and kind != "mfma" and dist < MFMA_VALU_RAW:
                     raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after MFMA {wi}")
-                if wk == "valu" and kind == "mfma" and dist < VALU_MFMA_RAW:
+                if wk in ("valu", "perm") and kind == "mfma" and dist < VALU_MFMA_RAW:
                     raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after VALU {wi}")
+                if wk in ("valu", "perm") and kind == "perm" and dist < PERM_RAW:
+                    raise AssertionError(f"{i}: {text}: swaps v{r} {dist} states after VALU {wi}")
                 if wk == "mfma" and kind == "mfma":
                     # only an exact accumulate chain (same registers as C) may follow an MFMA
                     role = [x[0] for x in reads if x[1] == r][0]
@@ -290,6 +435,23 @@ def main():
         nn = sum(x[4] for x in st.ins if x[1] == "nop")
         parts.append(f"// {prec}, {nt} tiles, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, {nm} MFMA, "
                      f"{nv} VALU, {nn} s_nop states")
+        parts.append(f"#define {name} \\")
+        parts.append(emit(st).replace("\n", " \\\n") + "")
+        parts.append("")
+    parts += [
+        "// 16x16x32 hidden layers for k_mlp16 (build_s16): the same interface and values; registers",
+        "// v0-v127 (accumulators v0-v63, B operands v64-v95, A operands v96-v111, biases v112-v127);",
+        "// %[vb0] = LDS byte address of the biases + 64 (lane >> 5), %[vb] = + 32 (lane >> 4).",
+        "",
+    ]
+    for name, prec, clamp in (("NR_S16_BF16_CLAMP", "bf16", True), ("NR_S16_BF16_MAX", "bf16", False),
+                              ("NR_S16_F16_MAX", "fp16", False)):
+        st = build_s16(prec, clamp)
+        nm = sum(1 for x in st.ins if x[1] == "mfma")
+        nv = sum(1 for x in st.ins if x[1] in ("valu", "perm"))
+        nn = sum(x[4] for x in st.ins if x[1] == "nop")
+        parts.append(f"// {prec}, 8 x 16-point tiles, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, "
+                     f"{nm} MFMA, {nv} VALU, {nn} s_nop states")
         parts.append(f"#define {name} \\")
         parts.append(emit(st).replace("\n", " \\\n") + "")
         parts.append("")
