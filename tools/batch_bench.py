@@ -26,6 +26,7 @@ ap.add_argument("--queues", type=int, default=8, help="nr_set_queue_shards")
 ap.add_argument("--temporal", type=int, default=0, help="nr_set_temporal_order")
 ap.add_argument("--debug", type=int, default=0, help="nr_set_debug flags (1024: frame-major batch queue)")
 ap.add_argument("--band", type=int, default=1, help="rows per band dealt round-robin (bench.py BAND)")
+ap.add_argument("--probe", default="0,16", help="nr_set_cost_probe max_steps,rays_per_wave (0: off)")
 ap.add_argument("--single", action="store_true",
                 help="time one-frame launches through nr_render_shard (the one-frame k_trace instance) "
                      "instead of nr_render_batch")
@@ -37,6 +38,7 @@ r.set_view(iv, nm, 0).set_static(1, 3).set_scene("v1").set_matcap(matcap)
 r.set_occupancy(a.bpc).set_wave_rays(a.rays).set_schedule(a.schedule)
 r.set_pixel_spread(a.spread).set_queue_shards(a.queues).set_temporal_order(a.temporal)
 r.set_debug(a.debug)
+r.set_cost_probe(*(int(v) for v in a.probe.split(",")))
 S = a.size
 bufs = [torch.zeros(S * S, dtype=torch.int32, device="cuda") for _ in range(32)]
 for n in (int(x) for x in a.shards.split(",")):
@@ -58,4 +60,4 @@ for n in (int(x) for x in a.shards.split(",")):
         r.synchronize()
         dt = (time.perf_counter() - t0) / (max(1, a.frames // b) * b) * 1e3
         line.append(f"{'single' if a.single and b == 1 else 'batch'} {b}: {dt:.3f} ms/frame")
-    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} debug {a.debug} band {a.band}: " + "  ".join(line), flush=True)
+    print(f"n={n} {a.precision} {S}^2 {a.schedule} bpc {a.bpc} rays {a.rays} spread {a.spread} queues {a.queues} temporal {a.temporal} probe {a.probe} debug {a.debug} band {a.band}: " + "  ".join(line), flush=True)
