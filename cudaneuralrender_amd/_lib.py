@@ -18,7 +18,7 @@ NR_COLOR_FACING, NR_COLOR_MATCAP = 0, 1
 NR_HOST, NR_DEVICE = 0, 1
 NR_SCHEDULE = {"persistent": 0, "wavefront": 1, "layered": 2}
 NR_GROUP_COPY, NR_GROUP_ASYNC = 1, 2
-NR_ENDGAME_DEFAULT = 0.0003  # include/neural_render.h: the bf16/fp16 endgame threshold by default
+NR_ENDGAME_DEFAULT = 0.001  # include/neural_render.h: the bf16/fp16 endgame threshold by default
 
 # every symbol include/neural_render.h declares
 EXPORTS = [

@@ -44,6 +44,7 @@ struct nr_ctx {
     uint16_t *d_lp16 = nullptr;
     uint16_t *d_x3lp = nullptr;  // bf16/fp16: the fp32x3 pack for the normals (MlpArgs::x3n)
     float *d_x3fl = nullptr;
+    int x3lp_bytes = 0, x3fl_bytes = 0;  // its sizes (TraceArgs: the EG instances stage it in LDS)
     bool fp32_normals = false;   // nr_set_debug bit 15: the bf16/fp16 tracers' normals in fp32 (A/B)
     float eg_tau = NR_ENDGAME_DEFAULT;  // nr_set_endgame: bf16/fp16 persistent renders' fp32x3 endgame
     float *d_lpf16 = nullptr;
@@ -91,6 +92,8 @@ struct nr_ctx {
     size_t cap_rays = 0;
     float4 *d_P[2] = {nullptr, nullptr}, *d_D[2] = {nullptr, nullptr};
     float4 *d_SP = nullptr, *d_SD = nullptr;
+    float4 *d_FP[2] = {nullptr, nullptr}, *d_FD[2] = {nullptr, nullptr};  // wavefront endgame: fine queues
+    size_t cap_fine = 0;
     size_t cap_ctr = 0;
     uint32_t *d_ctr = nullptr;       // [cap_ctr]: live counts per iteration, then shade count, then shade_it
     uint32_t *h_ctr = nullptr;       // pinned mirror
@@ -205,6 +208,7 @@ int upload_lowp(nr_ctx *c) {
     c->mlp16.lp_clamp = 0;
     dfree(c->d_x3lp); dfree(c->d_x3fl);
     c->mlp16.x3lp = nullptr; c->mlp16.x3fl = nullptr; c->mlp16.x3n = 0;
+    c->x3lp_bytes = 0; c->x3fl_bytes = 0;
     dfree(c->d_lps16); dfree(c->d_lpfs16);
     c->mlp16.lps = nullptr; c->mlp16.lpfs = nullptr;
     if (!c->fused || c->precision == NR_PRECISION_FP32) return NR_OK;
@@ -247,6 +251,7 @@ int upload_lowp(nr_ctx *c) {
         MlpArgs X{};
         if ((rc = upload_pack(c, xa, xf, c->d_x3lp, c->d_x3fl, X)) != NR_OK) return rc;
         c->mlp16.x3lp = X.lp; c->mlp16.x3fl = X.lpf;
+        c->x3lp_bytes = X.lp_bytes; c->x3fl_bytes = X.lpf_bytes;
         c->mlp16.x3n = c->fp32_normals ? 0 : 1;
     }
     return NR_OK;
@@ -303,6 +308,20 @@ int ensure_rays(nr_ctx *c, size_t n) {
     HIPCHK(c, hipMalloc(&c->d_SP, b));
     HIPCHK(c, hipMalloc(&c->d_SD, b));
     c->cap_rays = std::max<size_t>(n, 64);
+    return NR_OK;
+}
+
+// the wavefront schedule's fine queues (the endgame: rays marching in fp32x3), ping-pong
+int ensure_fine(nr_ctx *c, size_t n) {
+    if (n <= c->cap_fine) return NR_OK;
+    for (int i = 0; i < 2; ++i) { dfree(c->d_FP[i]); dfree(c->d_FD[i]); }
+    c->cap_fine = 0;
+    const size_t b = std::max<size_t>(n, 64) * sizeof(float4);
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(c, hipMalloc(&c->d_FP[i], b));
+        HIPCHK(c, hipMalloc(&c->d_FD[i], b));
+    }
+    c->cap_fine = std::max<size_t>(n, 64);
     return NR_OK;
 }
 
@@ -467,6 +486,10 @@ int upload_frames(nr_ctx *c, const nr_frame *frames, int nframes, size_t npix, i
 // rays of up to 32 frames share one queue; per iteration ONE k_march16 launch (mlp16 +
 // step + compaction) over it, at the end k_shade16.  The host polls the live count every
 // check_every iterations and stops early once it is 0.
+// bf16 / fp16 with the endgame (round 6, the persistent tracer's rule; endgame_tau): per
+// iteration the coarse pass (k_march16 mode 1) hands the rays whose 16-bit SDF is below tau to
+// the iteration's fine queue, then the fine pass (mode 2) marches that queue in fp32x3 -- so the
+// frames equal the persistent schedule's, bit for bit (tests/test_gpu_endgame.py).
 int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H, int band, int nshards, int shard,
                      int max_steps, int loc, nr_stats *stats, hipStream_t s) {
     const int rows = nr_shard_rows(H, band, nshards, shard);
@@ -481,9 +504,16 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
     // counters: (max_steps + 1) x [WF_SEGS live counts], [WF_SEGS shade counts], then
     // max_steps shade flags; each count on its own 128-byte line
     const size_t line = (size_t)WF_SEGS * 32;
-    const size_t nctr = (size_t)(max_steps + 2) * line + max_steps;
+    const float tau = endgame_tau(c, max_steps);
+    const bool eg = tau > 0.0f;
+    // the endgame's counters after them: (max_steps + 1) x [WF_SEGS fine counts], then one switch
+    // count per iteration
+    const size_t f_base = ((size_t)(max_steps + 2) * line + max_steps + line - 1) / line * line;
+    const size_t sw_base = f_base + (size_t)(max_steps + 1) * line;
+    const size_t nctr = eg ? sw_base + max_steps : (size_t)(max_steps + 2) * line + max_steps;
     int rc;
     if ((rc = ensure_rays(c, seg_cap * WF_SEGS)) != NR_OK) return rc;
+    if (eg && (rc = ensure_fine(c, seg_cap * WF_SEGS)) != NR_OK) return rc;
     if ((rc = ensure_ctr(c, nctr + 8)) != NR_OK) return rc;
     if ((rc = upload_frames(c, frames, nframes, npix, loc, chunk, s)) != NR_OK) return rc;
     RenderArgs A{};
@@ -505,6 +535,8 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
         Q.seg_cap = (long)seg_cap;
         Q.cnt_out = cnt; Q.p_out = c->d_P[0]; Q.d_out = c->d_D[0];
         Q.shade_cnt = shade_cnt; Q.shade_p = c->d_SP; Q.shade_d = c->d_SD; Q.shade_it = shade_it;
+        Q.eg_tau = tau;
+        uint32_t *fcnt = c->d_ctr + f_base, *fsw = c->d_ctr + sw_base;
         if ((rc = prof_begin(c, 0, s)) != NR_OK) return rc;
         HIPCHK(c, launch_init_f(A, F, Q, (long)npix, (long)total, cus * 8, s));
         if ((rc = prof_end(c, s)) != NR_OK) return rc;
@@ -514,15 +546,30 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
             Q.cnt_in = cnt + (size_t)it * line; Q.cnt_out = cnt + (size_t)(it + 1) * line;
             Q.p_in = c->d_P[it & 1]; Q.d_in = c->d_D[it & 1];
             Q.p_out = c->d_P[(it + 1) & 1]; Q.d_out = c->d_D[(it + 1) & 1];
+            // the endgame: the coarse pass appends this iteration's switched rays to fine queue `it`
+            // (where the previous fine pass left its survivors), the fine pass then marches it
+            Q.fcnt = fcnt + (size_t)it * line; Q.fp = c->d_FP[it & 1]; Q.fd = c->d_FD[it & 1]; Q.fsw = fsw + it;
             if ((rc = prof_begin(c, 1, s)) != NR_OK) return rc;
-            HIPCHK(c, launch_march16(A, mlp_for_frames(c, frames, nframes, 0), Q, F, c->precision, it, grid, s));
+            HIPCHK(c, launch_march16(A, mlp_for_frames(c, frames, nframes, 0), Q, F, c->precision, it, grid, s, eg ? 1 : 0));
             if ((rc = prof_end(c, s)) != NR_OK) return rc;
             ++tot.launches;
+            if (eg) {
+                QueueArgs G = Q;
+                G.cnt_in = fcnt + (size_t)it * line; G.cnt_out = fcnt + (size_t)(it + 1) * line;
+                G.p_in = c->d_FP[it & 1]; G.d_in = c->d_FD[it & 1];
+                G.p_out = c->d_FP[(it + 1) & 1]; G.d_out = c->d_FD[(it + 1) & 1];
+                if ((rc = prof_begin(c, 1, s)) != NR_OK) return rc;
+                HIPCHK(c, launch_march16(A, mlp_for_frames(c, frames, nframes, 0), G, F, c->precision, it, grid, s, 2));
+                if ((rc = prof_end(c, s)) != NR_OK) return rc;
+                ++tot.launches;
+            }
             if (c->check_every > 0 && (it + 1) % c->check_every == 0 && it + 1 < max_steps) {
                 HIPCHK(c, hipMemcpyAsync(c->h_ctr, Q.cnt_out, line * 4, hipMemcpyDeviceToHost, s));
+                if (eg) HIPCHK(c, hipMemcpyAsync(c->h_ctr + line, fcnt + (size_t)(it + 1) * line, line * 4,
+                                                 hipMemcpyDeviceToHost, s));
                 HIPCHK(c, hipStreamSynchronize(s));
                 uint64_t live = 0;
-                for (int q = 0; q < WF_SEGS; ++q) live += c->h_ctr[q * 32];
+                for (int q = 0; q < WF_SEGS; ++q) live += c->h_ctr[q * 32] + (eg ? c->h_ctr[line + q * 32] : 0u);
                 if (live == 0) break;
             }
         }
@@ -540,10 +587,18 @@ int render_wavefront(nr_ctx *c, const nr_frame *frames, int nframes, int W, int 
             const uint32_t *h = c->h_ctr;
             int iters = 0;
             for (int it = 0; it < max_steps; ++it) {
-                uint64_t live = 0;
+                uint64_t live = 0, fine = 0;
                 for (int q = 0; q < WF_SEGS; ++q) live += h[(size_t)it * line + q * 32];
-                tot.ray_steps += live;
                 if (it == 0) tot.rays_hit += live;
+                if (eg) {
+                    // the fine queue of iteration it: its switched rays (counted in `live` too: their
+                    // 16-bit evaluation) and the survivors of the previous fine pass
+                    for (int q = 0; q < WF_SEGS; ++q) fine += h[f_base + (size_t)it * line + q * 32];
+                    tot.endgame_evals += fine;
+                    tot.endgame_switches += h[sw_base + it];
+                    live += fine;
+                }
+                tot.ray_steps += live;
                 if (live) iters = std::max(iters, it + 1);
                 if (h[(size_t)(max_steps + 2) * line + it]) iters = std::max(iters, std::min(it + 2, max_steps));
             }
@@ -774,7 +829,7 @@ int nr_destroy(nr_ctx *c) {
     (void)hipSetDevice(c->device);
     if (!(c->use_own && !c->own_stream)) (void)hipStreamSynchronize(c->stream);
     free_network(c);
-    for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); }
+    for (int i = 0; i < 2; ++i) { dfree(c->d_P[i]); dfree(c->d_D[i]); dfree(c->d_FP[i]); dfree(c->d_FD[i]); }
     dfree(c->d_SP); dfree(c->d_SD); dfree(c->d_ctr); dfree(c->d_out); dfree(c->d_tr); dfree(c->d_stamps); dfree(c->d_bcost); dfree(c->d_order[0]); dfree(c->d_order[1]); dfree(c->d_io); dfree(c->d_matcap);
     dfree(c->d_rargs); dfree(c->d_lsdf); dfree(c->d_lz);
     dfree(c->d_frames); dfree(c->d_bout);
@@ -990,6 +1045,8 @@ int nr_render_batch(nr_ctx *c, const nr_frame *frames, int nframes, int W, int H
         // 0.334; profiles/r2_ab_experiments.txt (10)).  Debug bit 10: frame-major (A/B).
         T.interleave = !((c->debug >> 10) & 1);
         T.eg_tau = endgame_tau(c, max_steps);
+        T.x3lp_bytes = c->x3lp_bytes;
+        T.x3fl_bytes = c->x3fl_bytes;
         // the counters restart for every launch; the statistics accumulate
         HIPCHK(c, hipMemsetAsync(c->d_tr, 0, f0 == 0 ? tr_bytes : (size_t)NR_MAX_QUEUES * 128, s));
         // workgroups per CU: default_bpc (with several frames in a launch their tails overlap,
@@ -1123,6 +1180,8 @@ int nr_render_shard(nr_ctx *c, uint32_t *out, int W, int H, int band, int nshard
         T.itmap = (c->debug & 8) != 0;
         // the stamps instance (nr_set_debug bit 0) marches without the endgame
         T.eg_tau = (c->debug & 1) ? 0.0f : endgame_tau(c, max_steps);
+        T.x3lp_bytes = c->x3lp_bytes;
+        T.x3fl_bytes = c->x3fl_bytes;
         {
             const int sp = spread_for(c, 1, npix);
             T.spread_shift = sp > 1 ? 31 - __builtin_clz((unsigned)sp) : 0;

@@ -10,6 +10,13 @@
 #ifndef NR_TRACE_BPC_EG
 #define NR_TRACE_BPC_EG 3
 #endif
+// Waves per workgroup of the endgame instances (round 6): 12 -- one workgroup per CU, the same 3
+// waves per SIMD -- so that one LDS copy of the fp32x3 pack (~31 KB, read by the fine passes and
+// the normals) fits beside the 16-bit pack and the 12 waves' queues; 4 = round 5's form (three
+// 4-wave workgroups per CU, the fp32x3 weights read from global memory / L2)
+#ifndef NR_EG_WAVES
+#define NR_EG_WAVES 12
+#endif
 
 namespace nr {
 
@@ -71,6 +78,13 @@ struct QueueArgs {
     uint32_t *shade_it;     // per-iteration count of waves that enqueued converged rays
     long seg_cap;           // segmented queues (wavefront schedule): WF_SEGS segments of
                             // seg_cap entries, one counter each (cnt_*[s], shade_cnt[s])
+    // the endgame on the wavefront schedule (round 6; bf16/fp16): the coarse pass appends the rays
+    // whose 16-bit SDF falls below eg_tau, unstepped, to this iteration's fine queue (fcnt, fp, fd;
+    // segmented like the live queue) and counts them in *fsw
+    uint32_t *fcnt;
+    float4 *fp, *fd;
+    uint32_t *fsw;
+    float eg_tau;
 };
 constexpr int WF_SEGS = 8;
 
@@ -128,6 +142,8 @@ struct TraceArgs {
     double inv_nframes;         // 1 / nframes for udiv_r
     float eg_tau;               // bf16/fp16 with an fp32x3 pack: the endgame's switch threshold (0 = off;
                                 // k_trace's EG instances, nr_set_endgame)
+    int x3lp_bytes, x3fl_bytes; // sizes of the fp32x3 pack (16-byte multiples): the endgame
+                                // instances stage it in LDS beside the 16-bit pack (NR_EG_WAVES)
 };
 
 int dense_lds_bytes(int in, int out);
@@ -135,7 +151,7 @@ hipError_t launch_dense(const DenseArgs &D, int src, int grid, hipStream_t st);
 hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArgs &Q, long npix, long total,
                          int grid, hipStream_t st);
 hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
-                          int it, int grid, hipStream_t st);
+                          int it, int grid, hipStream_t st, int mode = 0);
 hipError_t launch_shade16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int grid,
                           hipStream_t st);
 hipError_t launch_set_args(const RenderArgs &A, RenderArgs *d, hipStream_t st);

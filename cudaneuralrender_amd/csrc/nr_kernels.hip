@@ -445,6 +445,9 @@ __device__ __forceinline__ QueueArgs seg_view(const QueueArgs &Q, int s) {
     V.shade_cnt = Q.shade_cnt + s * WF_CSTRIDE;
     V.shade_p = Q.shade_p + s * Q.seg_cap;
     V.shade_d = Q.shade_d + s * Q.seg_cap;
+    V.fcnt = Q.fcnt + s * WF_CSTRIDE;
+    V.fp = Q.fp + s * Q.seg_cap;
+    V.fd = Q.fd + s * Q.seg_cap;
     return V;
 }
 
@@ -489,7 +492,14 @@ __global__ __launch_bounds__(256) void k_init_f(RenderArgs A, const FrameArgs *_
 // One iteration over the queue: 64 rays per wave through mlp16 (4 x 16-point tiles, the
 // k_trace / k_mlp16 MLP), then the step and the block-aggregated compaction into the
 // ray's segment.  Blocks take 256-ray work units over the segments, grid-stride.
-template <int PREC>
+// The endgame (round 6, bf16/fp16; nr_set_endgame, the persistent tracer's EG rule restated on
+// queues): MODE 1 = the coarse pass -- a ray whose 16-bit MLP output is below Q.eg_tau goes,
+// unstepped, to this iteration's fine queue; MODE 2 = the fine pass over that queue -- the fp32x3
+// MLP on every point (mlp16_x3_normal: the split within the x3 pack's bounds, the fp32 MLP
+// outside), then the same step, survivors to the next iteration's fine queue.  So every ray takes
+// one step per iteration, the switch iteration's and all later ones in fp32x3, as in k_trace and
+// the oracle (or_set_endgame).
+template <int PREC, int MODE = 0>
 __global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueArgs Q, const FrameArgs *__restrict__ F,
                                                  int it) {
     Smem16 S = stage16<PREC, false>(M);
@@ -507,8 +517,21 @@ __global__ __launch_bounds__(256) void k_march16(RenderArgs A, MlpArgs M, QueueA
         const long rem = n_s - (off + 64 * wv);
         const uint32_t tmask = rem >= 64 ? 0xfu : (rem <= 0 ? 0u : (1u << ((rem + 15) >> 4)) - 1u);
         float sdf = 0.0f;
-        if (tmask) sdf = mlp16(M, S.s32, S.slp, S.sfl, PREC, F[f].frame_f, sp.x, sp.y, sp.z, tmask, M.lp_clamp != 0);
-        march_rays(A, seg_view(Q, s), it, live, sp, sd, sdf, F[f].zoff);
+        if constexpr (MODE == 2) {
+            if (tmask) sdf = mlp16_x3_normal<false>(M, S.s32, M.x3lp, M.x3fl, F[f].frame_f, sp.x, sp.y, sp.z, tmask);
+        } else {
+            if (tmask) sdf = mlp16(M, S.s32, S.slp, S.sfl, PREC, F[f].frame_f, sp.x, sp.y, sp.z, tmask, M.lp_clamp != 0);
+        }
+        const QueueArgs V = seg_view(Q, s);
+        if constexpr (MODE == 1) {
+            const bool sw = live && sdf < Q.eg_tau;
+            march_rays(A, V, it, live && !sw, sp, sd, sdf, F[f].zoff);
+            const Slots sl = block_append2(sw, V.fcnt, false, nullptr);
+            if (sw) { V.fp[sl.a] = sp; V.fd[sl.a] = sd; }
+            if (threadIdx.x == 0 && sl.na) atomicAdd(Q.fsw, sl.na);
+        } else {
+            march_rays(A, V, it, live, sp, sd, sdf, F[f].zoff);
+        }
     }
 }
 
@@ -610,9 +633,17 @@ hipError_t launch_init_f(const RenderArgs &A, const FrameArgs *F, const QueueArg
     return hipGetLastError();
 }
 hipError_t launch_march16(const RenderArgs &A, const MlpArgs &M, const QueueArgs &Q, const FrameArgs *F, int prec,
-                          int it, int grid, hipStream_t st) {
+                          int it, int grid, hipStream_t st, int mode) {
     const int sm = smem16_bytes(M, prec, false);
-    if (prec == NR_PRECISION_BF16)
+    if (mode == 1 && prec == NR_PRECISION_BF16)
+        hipLaunchKernelGGL((k_march16<NR_PRECISION_BF16, 1>), dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (mode == 1 && prec == NR_PRECISION_FP16)
+        hipLaunchKernelGGL((k_march16<NR_PRECISION_FP16, 1>), dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (mode == 2 && prec == NR_PRECISION_BF16)
+        hipLaunchKernelGGL((k_march16<NR_PRECISION_BF16, 2>), dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (mode == 2 && prec == NR_PRECISION_FP16)
+        hipLaunchKernelGGL((k_march16<NR_PRECISION_FP16, 2>), dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
+    else if (prec == NR_PRECISION_BF16)
         hipLaunchKernelGGL(k_march16<NR_PRECISION_BF16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);
     else if (prec == NR_PRECISION_FP16)
         hipLaunchKernelGGL(k_march16<NR_PRECISION_FP16>, dim3(grid), dim3(256), sm, st, A, M, Q, F, it);

@@ -1031,15 +1031,36 @@ __device__ __forceinline__ Smem16 stage16(const MlpArgs &M) {
         dst = reinterpret_cast<int4 *>(S.sfl);
         for (int i = threadIdx.x; i < M.lpf_bytes / 16; i += blockDim.x) dst[i] = src[i];
     }
+
     __syncthreads();
     return S;
 }
 
+// The fp32x3 pack copied into dynamic LDS after the 16-bit pack (the endgame instances with
+// NR_EG_WAVES > 4, whose fine passes and normals read it there); before stage16, whose
+// __syncthreads completes it.  Returns the LDS copies of M.x3lp / M.x3fl.
+template <int PREC>
+__device__ __forceinline__ void stage_x3(const MlpArgs &M, int x3lp_bytes, int x3fl_bytes, const uint16_t *&xl,
+                                         const float *&xf) {
+    const int off = (PREC == NR_PRECISION_FP32 ? M.pk_bytes : 0) + M.lp_bytes + M.lpf_bytes;
+    uint16_t *l = reinterpret_cast<uint16_t *>(nr_smem16 + off);
+    float *f = reinterpret_cast<float *>(nr_smem16 + off + x3lp_bytes);
+    const int4 *src = reinterpret_cast<const int4 *>(M.x3lp);
+    int4 *dst = reinterpret_cast<int4 *>(l);
+    for (int i = threadIdx.x; i < x3lp_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    src = reinterpret_cast<const int4 *>(M.x3fl);
+    dst = reinterpret_cast<int4 *>(f);
+    for (int i = threadIdx.x; i < x3fl_bytes / 16; i += blockDim.x) dst[i] = src[i];
+    xl = l;
+    xf = f;
+}
+
 // host side: the dynamic LDS stage16<prec, need32> uses
-inline int smem16_bytes(const MlpArgs &M, int prec, bool need32) {
+inline int smem16_bytes(const MlpArgs &M, int prec, bool need32, int x3_bytes = 0) {
     (void)need32;
     const bool lds32 = prec == NR_PRECISION_FP32;
-    return (lds32 ? M.pk_bytes : 0) + (prec != NR_PRECISION_FP32 ? M.lp_bytes + M.lpf_bytes : 0);
+    return (lds32 ? M.pk_bytes : 0) + (prec != NR_PRECISION_FP32 ? M.lp_bytes + M.lpf_bytes : 0) +
+           x3_bytes;
 }
 
 }  // namespace nr

@@ -206,7 +206,7 @@ __device__ __forceinline__ void set_priority(int prio) {
 // profiles/r5_ab_eg.txt)
 // (NR_TRACE_BPC_EG: nr_kernels.h, where the host side caps the grid with it)
 template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false>
-__global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
+__global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
                                   : PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                   : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
                                   : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
@@ -230,28 +230,35 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             reinterpret_cast<uint32_t *>(sf + f)[w] = w < 12 ? src[w] : (w < 16 ? src[16 + w] : (w == 16 ? src[32] : 0u));
         }
     }
-    Smem16 S = stage16<PREC, true>(M);  // (its __syncthreads also covers sf)
+    // waves per workgroup: 4, or NR_EG_WAVES for the endgame instances, which then hold the fp32x3
+    // pack in LDS (X3L) for their fine passes and normals
+    constexpr int NW = EG ? NR_EG_WAVES : 4;
+    constexpr bool X3L = EG && NR_EG_WAVES > 4;
+    const uint16_t *x3l = M.x3lp;
+    const float *x3f = M.x3fl;
+    if constexpr (X3L) stage_x3<PREC>(M, T.x3lp_bytes, T.x3fl_bytes, x3l, x3f);
+    Smem16 S = stage16<PREC, true>(M);  // (its __syncthreads also covers sf and the fp32x3 copy)
     // converged rays per wave: {p.xyz, pixel} and the frame (the direction is regenerated from
     // the pixel for facingColor; matCapColor does not read it): 21 instead of 42 KB per CU,
     // so that 4 fp32 workgroups share a CU
-    __shared__ float4 stash[4][STASH];
-    __shared__ uint8_t stash_f[4][BATCH ? STASH : 1];
+    __shared__ float4 stash[NW][STASH];
+    __shared__ uint8_t stash_f[NW][BATCH ? STASH : 1];
     // DENSE: per wave a ring of RB generated rays {p.xyz, tfar}, {d.xyz, pixel} (+ frame), as two
     // arrays of 16-byte entries so that consecutive lanes' ds_write_b128 / ds_read_b128 stay
     // conflict-free: 64 rays, 8.25 KB per workgroup (the fp32 tracer's ring, an A/B build option,
     // holds 16: its 4 workgroups per CU have 2 KB of LDS left each)
     constexpr int RB = PREC == NR_PRECISION_FP32 ? 16 : NR_RING_LOWP;
-    __shared__ float4 rbuf_p[DENSE ? 4 : 1][DENSE ? RB : 1], rbuf_d[DENSE ? 4 : 1][DENSE ? RB : 1];
-    __shared__ uint8_t rbuf_f[DENSE && BATCH ? 4 : 1][DENSE && BATCH ? RB : 1];
+    __shared__ float4 rbuf_p[DENSE ? NW : 1][DENSE ? RB : 1], rbuf_d[DENSE ? NW : 1][DENSE ? RB : 1];
+    __shared__ uint8_t rbuf_f[DENSE && BATCH ? NW : 1][DENSE && BATCH ? RB : 1];
     // each lane's marching ray {d.xyz, pixel} (DLDS): 4 KB per workgroup
     constexpr bool DLDS = DENSE && NR_RAY_D_LDS;
-    __shared__ float4 ray_dp[DLDS ? 4 : 1][DLDS ? 64 : 1];
+    __shared__ float4 ray_dp[DLDS ? NW : 1][DLDS ? 64 : 1];
     // EG: per wave the fine queue {p.xyz, tfar}, {d.xyz, pixel}, iteration | frame << 24: a pass
     // leaves fewer than 32 rays (or none), one iteration adds at most 64
     static_assert(!EG || (DLDS && NX3 && (PREC == NR_PRECISION_BF16 || PREC == NR_PRECISION_FP16)), "EG instances");
     constexpr int FQ = EG ? 32 - 1 + 64 : 1;
-    __shared__ float4 fq_p[EG ? 4 : 1][FQ], fq_d[EG ? 4 : 1][FQ];
-    __shared__ uint32_t fq_i[EG ? 4 : 1][FQ];
+    __shared__ float4 fq_p[EG ? NW : 1][FQ], fq_d[EG ? NW : 1][FQ];
+    __shared__ uint32_t fq_i[EG ? NW : 1][FQ];
     int nfq = 0;        // rays in the wave's fine queue (EG)
     uint32_t nfine = 0;  // fp32x3 march evaluations (EG)
     uint32_t nswitch = 0;  // rays handed to the fine queue (EG; wave-uniform)
@@ -272,7 +279,8 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
     const int q4 = lane & 3;
     int nstash = 0;
     const int nq = 1 << T.nq_shift;  // pixel-queue shards
-    int shard = blockIdx.x & (nq - 1), tries = 0;
+    // a 12-wave endgame workgroup spreads its waves over 3 shards, as three 4-wave ones did
+    int shard = (NW > 4 ? (int)(blockIdx.x * (NW / 4) + (threadIdx.x >> 8)) : (int)blockIdx.x) & (nq - 1), tries = 0;
     bool qempty = false;
     uint32_t pool_base = 0, pool_cnt = 0, pend_v = 0;  // NR_QUEUE_PREFETCH state
     bool pend = false;
@@ -589,7 +597,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
             // the shading loop into registers held for the kernel's life
             int zoff_x3 = 0;
             if constexpr (NX3) asm volatile("" : "+s"(zoff_x3));
-            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, M.x3lp + zoff_x3, M.x3fl + zoff_x3, fr_of(sfr), pq.x, pq.y,
+            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, (X3L ? x3l : M.x3lp) + zoff_x3, (X3L ? x3f : M.x3fl) + zoff_x3, fr_of(sfr), pq.x, pq.y,
                                                     pq.z, smask)
                                   : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
@@ -635,7 +643,7 @@ __global__ __launch_bounds__(256, EG ? NR_TRACE_BPC_EG
                 int zx = 0;
                 asm volatile("" : "+s"(zx));
                 // (one two-tile pass: C3 batch 1.85 -> 1.72 ms against two one-tile passes)
-                const float fsdf = mlp16_x3_normal<false>(M, S.s32, M.x3lp + zx, M.x3fl + zx, fr_of(ff), fp.x, fp.y, fp.z,
+                const float fsdf = mlp16_x3_normal<false>(M, S.s32, (X3L ? x3l : M.x3lp) + zx, (X3L ? x3f : M.x3fl) + zx, fr_of(ff), fp.x, fp.y, fp.z,
                                                           nb > 32 ? 0xfu : 0x3u);
                 nfine += (uint32_t)nb;
                 nsteps += (uint32_t)nb;
@@ -1129,8 +1137,13 @@ static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const Tr
     if constexpr (LOWP && !PROBE) {
         if constexpr (!STAMPS) {
             if (M.x3n && T.eg_tau > 0.0f) {
-                // the grid is at most NR_TRACE_BPC_EG workgroups per CU (nr_api.hip trace_bpc)
-                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(grid), dim3(256), sm, st, A, M, T);
+                // the grid is at most NR_TRACE_BPC_EG 4-wave workgroups per CU (nr_api.hip trace_bpc):
+                // as NR_EG_WAVES-wave workgroups, one per CU, with the fp32x3 pack in their LDS
+                constexpr int G = NR_EG_WAVES / 4;
+                const int g = std::max(1, (grid + G - 1) / G);
+                const int smx = NR_EG_WAVES > 4 ? smem16_bytes(M, PREC, true, T.x3lp_bytes + T.x3fl_bytes) : sm;
+                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(g), dim3(64 * NR_EG_WAVES), smx, st,
+                                   A, M, T);
                 return hipGetLastError();
             }
         }

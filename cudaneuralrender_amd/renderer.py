@@ -274,7 +274,7 @@ class Renderer:
 
     def set_endgame(self, tau):
         """nr_set_endgame: bf16/fp16 rays whose 16-bit MLP output falls below tau finish their
-        march in fp32x3 (default NR_ENDGAME_DEFAULT = 3e-4; 0 = the pure 16-bit march)."""
+        march in fp32x3 (default NR_ENDGAME_DEFAULT = 1e-3; 0 = the pure 16-bit march)."""
         self._chk(self._L.nr_set_endgame(self._ctx, float(tau)))
         return self
 

@@ -160,8 +160,8 @@ def test_endgame_four_input_network_frame_bound():
     assert any((i != 0).any() for i in imgs)
 
 
-def test_endgame_off_for_fp32_normals_and_other_schedules(chrome):
-    """Bit 15 (fp32 normals) and the wavefront schedule march in pure 16-bit (no fp32x3 pass)."""
+def test_endgame_off_for_fp32_normals(chrome):
+    """Bit 15 (fp32 normals) marches in pure 16-bit (no fp32x3 pass), on both schedules."""
     with nr.Renderer(0) as r:
         r.load_h5(nr.geometry_path("plane_1")).set_precision("bf16")
         iv, nm = nr.camera(0.0, 0.0, 2.0)
@@ -169,9 +169,40 @@ def test_endgame_off_for_fp32_normals_and_other_schedules(chrome):
         r.set_debug(1 << 15)
         _, st = r.render(96, 96, 64)
         assert st["endgame_evals"] == 0
-        r.set_debug(0).set_schedule("wavefront")
+        r.set_schedule("wavefront")
         _, st = r.render(96, 96, 64)
         assert st["endgame_evals"] == 0
+
+
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+def test_endgame_wavefront_equals_persistent(chrome, prec):
+    """Round 6: the wavefront schedule's endgame (a fine queue per iteration, k_march16 modes 1 / 2)
+    gives the persistent tracer's frames, ray-step, fp32x3-evaluation and switch counts -- single
+    frames and a batch, against the oracle too."""
+    net = _oracle("car_1")
+    cams = [nr.camera(5.0 * i - 10.0, 37.0 * i + 20.0, 2.2) + (i,) for i in range(3)]
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("car_1")).set_precision(prec)
+        r.set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        pers = []
+        for iv, nm, f in cams:
+            r.set_view(iv, nm, f)
+            pers.append(r.render(136, 120, 128))
+        pb, pbs = r.render_batch(136, 120, cams, 128)
+        r.set_schedule("wavefront")
+        wave = []
+        for iv, nm, f in cams:
+            r.set_view(iv, nm, f)
+            wave.append(r.render(136, 120, 128))
+        wb, wbs = r.render_batch(136, 120, cams, 128)
+    for (iv, nm, f), (a, sa), (b, sb), c, d in zip(cams, pers, wave, pb, wb):
+        ref, rst = net.render(136, 120, iv, nm, frame=f, color_type=1, matcap=chrome, max_steps=128, nthreads=16,
+                              precision=PREC[prec], endgame=nr.NR_ENDGAME_DEFAULT)
+        assert np.array_equal(b, ref) and np.array_equal(a, ref) and np.array_equal(d, ref) and np.array_equal(c, ref)
+        for k in ("ray_steps", "endgame_evals", "endgame_switches", "rays_shaded"):
+            assert sa[k] == sb[k] == rst[k], (k, sa[k], sb[k], rst[k])
+    for k in ("ray_steps", "endgame_evals", "endgame_switches"):
+        assert pbs[k] == wbs[k] > 0, (k, pbs[k], wbs[k])
 
 
 def test_endgame_rejects_bad_threshold():
@@ -183,9 +214,9 @@ def test_endgame_rejects_bad_threshold():
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_schedule_pixel_contract(chrome, prec):
-    """The documented per-schedule rule for 16-bit frames at default settings (neural_render.h,
-    nr_set_schedule): persistent = the endgame frame, wavefront = the persistent frame with
-    nr_set_endgame(0) (the pure 16-bit march), layered = the fp32 frame; each against the oracle."""
+    """The documented per-schedule rule for 16-bit frames (neural_render.h, nr_set_schedule): at
+    default settings persistent = wavefront = the endgame frame, with nr_set_endgame(0) both = the
+    pure 16-bit march, layered = the fp32 frame; each against the oracle."""
     net = _oracle("plane_1")
     iv, nm = nr.camera(-12.0, 35.0, 2.1)
     kw = dict(color_type=1, matcap=chrome, max_steps=128, nthreads=16)
@@ -199,9 +230,11 @@ def test_schedule_pixel_contract(chrome, prec):
         lay, _ = r.render(128, 120, 128)
         r.set_schedule("persistent").set_endgame(0)
         pure, _ = r.render(128, 120, 128)
+        r.set_schedule("wavefront")
+        wpure, _ = r.render(128, 120, 128)
     ref_eg, _ = net.render(128, 120, iv, nm, precision=PREC[prec], endgame=nr.NR_ENDGAME_DEFAULT, **kw)
     ref_pure, _ = net.render(128, 120, iv, nm, precision=PREC[prec], **kw)
     ref_f32, _ = net.render(128, 120, iv, nm, precision=0, **kw)
-    assert np.array_equal(pers, ref_eg)
-    assert np.array_equal(wave, pure) and np.array_equal(wave, ref_pure)
+    assert np.array_equal(pers, ref_eg) and np.array_equal(wave, ref_eg)
+    assert np.array_equal(pure, ref_pure) and np.array_equal(wpure, ref_pure)
     assert np.array_equal(lay, ref_f32)

@@ -82,9 +82,8 @@ def contract(name, geom, size, steps, prec, rows, chrome, record, tau=0.0):
     # >= 0.98 for every C5 crop)
     x = res["vs_exact_mlp"]
     if tau > 0:
-        ri, riou, rmean = EXACT_EG_R5[(name, geom)]
-        assert x["iou"] >= EG_IOU_TARGET[name], res
-        assert x["identical"] >= ri - 0.02 and max(x["mean_abs"][:3]) <= 1.25 * rmean, res
+        ti, tiou, tmean = EG_TARGETS[(name, geom)]
+        assert x["identical"] >= ti and x["iou"] >= tiou and max(x["mean_abs"][:3]) <= tmean, res
         # and never worse than the pure march's r4 figures
         assert x["identical"] >= EXACT_R4[(name, geom)][0] and x["iou"] >= EXACT_R4[(name, geom)][1], res
     else:
@@ -102,16 +101,19 @@ def contract(name, geom, size, steps, prec, rows, chrome, record, tau=0.0):
 
 # (identical, IoU, max per-channel mean |delta|) against the exact-MLP frame
 EXACT_BOUND = {"bf16": (0.72, 0.90, 12.0), "fp16": (0.75, 0.78, 3.6)}
-# with the endgame at NR_ENDGAME_DEFAULT = 3e-4 (round 5, profiles/r5_lowp_contract.json): coverage IoU to
-# VERDICT r4's targets, identical pixels and mean |delta| within 2 points / 1.25x of the measured
-EG_IOU_TARGET = {"C3": 0.99, "C4": 0.99, "C5": 0.98}
-EXACT_EG_R5 = {("C3", "car_1"): (0.7775, 0.99986, 2.2983),
-               ("C4", "plane_2"): (0.8843, 0.99827, 6.37),
-               ("C5", "plane_1"): (0.901, 0.99713, 2.3742),
-               ("C5", "plane_2"): (0.9316, 0.99984, 2.1632),
-               ("C5", "plane_3"): (0.9961, 0.99776, 0.9795),
-               ("C5", "car_1"): (0.7725, 0.9998, 1.99),
-               ("C5", "3a3d4a90a2db90b4203936772104a82d.obj"): (0.8824, 0.99815, 2.2141)}
+# with the endgame (NR_ENDGAME_DEFAULT): FIXED targets, not measured-minus-epsilon
+# floors -- C3 identical >= 0.77, C4 identical >= 0.88 and mean |delta| <= 5.0 (what tau = 1e-3 gave in
+# round 5), coverage IoU >= 0.99 (C3, C4) / 0.98 (C5), the C5 crops' identical / mean |delta|
+# floors as round 5 set them (its 3e-4 figures - 0.02 / x1.25).  The default threshold is the one that
+# meets them all: 1e-3 (C4's mean |delta| 6.37 at 3e-4, 5.59 at 5e-4, 5.03 at 7e-4, 4.57 at 1e-3 on the
+# oracle's CPU restatement of the same crop, profiles/r6_endgame_tau.txt).
+EG_TARGETS = {("C3", "car_1"): (0.77, 0.99, 3.0),
+              ("C4", "plane_2"): (0.88, 0.99, 5.0),
+              ("C5", "plane_1"): (0.881, 0.98, 2.968),
+              ("C5", "plane_2"): (0.9116, 0.98, 2.704),
+              ("C5", "plane_3"): (0.9761, 0.98, 1.224),
+              ("C5", "car_1"): (0.7525, 0.98, 2.488),
+              ("C5", "3a3d4a90a2db90b4203936772104a82d.obj"): (0.8624, 0.98, 2.768)}
 EXACT_R4 = {("C3", "car_1"): (0.7398, 0.99801, 5.629), ("C4", "plane_2"): (0.8367, 0.93107, 10.447),
             ("C5", "plane_1"): (0.8543, 0.86754, 3.266), ("C5", "plane_2"): (0.9205, 0.97787, 2.978),
             ("C5", "plane_3"): (0.9922, 0.81736, 1.412), ("C5", "car_1"): (0.7634, 0.99674, 2.687),

@@ -7,4 +7,4 @@ TAG=${1:?tag}
 O=gpurun_out
 timeout -k 10 900 bash tools/profile_round.sh $TAG > $O/profile_round_$TAG.log 2>&1 &&
 EG=0 timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16_$TAG bf16 3 > $O/pmc_bf16_$TAG.txt 2>&1 &&
-EG=0.0003 timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16eg_$TAG bf16 3 > $O/pmc_bf16eg_$TAG.txt 2>&1
+EG=0.001 timeout -k 10 400 bash tools/pmc_lowp.sh $O/pmc_bf16eg_$TAG bf16 3 > $O/pmc_bf16eg_$TAG.txt 2>&1
