@@ -176,6 +176,28 @@ __device__ __forceinline__ void set_priority(int prio) {
     }
 }
 
+// k_trace's arguments re-read from the kernarg segment (scalar loads) where a phase uses them,
+// instead of being held in SGPRs -- or spilled to VGPR lanes, one v_readlane per use -- across the
+// whole loop.  The pointer is made opaque per use, so the loads cannot be
+// hoisted out of the loop.  The struct mirrors the kernarg layout of k_trace(A, M, T): each
+// argument at its natural alignment, in order (the code object metadata, llvm-readelf --notes:
+// by_value arguments at offsets 0, 200 and 304; every GPU parity test reads through it).
+// (SGPRs spilled to VGPR lanes: the bf16 batched tracer with fp32x3 normals 124 -> 59, its endgame
+// instance 151 -> 51, the fp32 batched tracer 85 -> 8.)
+#ifndef NR_ARG_RELOAD
+#define NR_ARG_RELOAD 1
+#endif
+struct TraceKargs {
+    RenderArgs A;
+    MlpArgs M;
+    TraceArgs T;
+};
+__device__ __forceinline__ const TraceKargs *fresh_kargs() {
+    auto p = (const __attribute__((address_space(4))) TraceKargs *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (const TraceKargs *)p;
+}
+
 // PROBE: the cost-probe pre-pass (TraceArgs::probe) -- one ray per 8x8 block, at most
 // T.take rays per wave, no pixels written; each block's bcost gets its probe ray's
 // iteration count (max_steps is the probe's cap).
@@ -322,6 +344,11 @@ __global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
         NR_PHASE(refill);
         // ---- refill free slots from the pixel queue
         if (!qempty || (DENSE && rb_n > 0)) {
+#if NR_ARG_RELOAD
+            const TraceKargs *K = fresh_kargs();
+            const RenderArgs &A = K->A;
+            const TraceArgs &T = K->T;
+#endif
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
             const uint64_t freem = __ballot(it < 0) & T.lane_cap;
@@ -577,6 +604,11 @@ __global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
         constexpr int SHR = PREC == NR_PRECISION_FP32 ? 16 : NR_SHADE_RAYS_LOWP;  // rays per shading pass
         bool fpass = false;  // EG: a fine pass ran in this iteration
         while (true) {
+#if NR_ARG_RELOAD
+            const TraceKargs *K = fresh_kargs();
+            const RenderArgs &A = K->A;
+            const TraceArgs &T = K->T;
+#endif
         while (nstash >= SHR || (drained && nstash > 0 && !lm && nfq == 0)) {
             const int nb = min(SHR, nstash);
             const int k = lane >> 2;
@@ -738,6 +770,11 @@ __global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
         if (MLP_PRIO) set_priority(MLP_PRIO);
         const float sdf = mlp16(M, S.s32, S.slp, S.sfl, prec, fr_of(rf), p.x, p.y, p.z, tmask, M.lp_clamp != 0);
         NR_PHASE(step);
+#if NR_ARG_RELOAD
+        const TraceKargs *K = fresh_kargs();
+        const RenderArgs &A = K->A;
+        const TraceArgs &T = K->T;
+#endif
         if constexpr (timing) {
             // iterations with <= 4 rays (low word) and ray-steps (high word) after the drain; the
             // live rays when the wave first saw the queue drained
