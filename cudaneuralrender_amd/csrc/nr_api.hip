@@ -1360,7 +1360,8 @@ int nr_mlp_forward(nr_ctx *c, const float *X, float *Y, long n, int loc) {
         const int grid = num_cus(c->device) * bpc;
         if (c->debug & 64)  // diagnostic: n = repetitions, X >= 64 points, Y >= 65 floats
             HIPCHK(c, launch_mlp_latency(c->mlp16, c->precision, dX, dY, (int)n,
-                                         ((c->wave_rays > 0 ? c->wave_rays : 64) + 15) / 16, (c->debug >> 7) & 1, s));
+                                         ((c->wave_rays > 0 ? c->wave_rays : 64) + 15) / 16,
+                                         ((c->debug >> 7) & 1) | (((c->debug >> 13) & 3) << 1), s));
             // (bf16/fp16: wave_rays 16 / 32 time the tracer's 64-point form on 1 / 2 32-point tiles,
             // otherwise the 128-point form)
         else

@@ -10,9 +10,12 @@ extern __shared__ __attribute__((aligned(16))) unsigned char nr_smem_diag[];
 // Latency of the fp32 MLP on NT tiles for one wave alone on its SIMD (nr_set_debug
 // bit 6): `reps` back-to-back evaluations, each input depending on the previous output.
 // Y[0] = shader cycles per evaluation, Y[1..64] = the last outputs.  PART: see
-// mlp16_fp32_nt.
-template <int NT, int PART>
-__global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
+// mlp16_fp32_nt.  CL: the clamped ReLU form (the tracer's, on the scaled pack); NH: unrolled
+// for 7 hidden layers.
+// (at most 128 VGPRs, the tracers' budget, so that the register allocation -- how far ahead the
+// unrolled form can request weights -- is theirs)
+template <int NT, int PART, bool CL = false, int NH = 0>
+__global__ __launch_bounds__(64, 4) void k_mlp_latency(MlpArgs M, const float *__restrict__ X, float *__restrict__ Y,
                                                     int reps) {
     float *s32 = reinterpret_cast<float *>(nr_smem_diag);
     const int4 *src = reinterpret_cast<const int4 *>(M.pk);
@@ -22,7 +25,7 @@ __global__ __launch_bounds__(64) void k_mlp_latency(MlpArgs M, const float *__re
     float x = X[3 * lane], y = X[3 * lane + 1], z = X[3 * lane + 2], v = 0.0f;
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    for (int r = 0; r < reps; ++r) v = mlp16_fp32_nt<NT, PART>(s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
+    for (int r = 0; r < reps; ++r) v = mlp16_fp32_nt<NT, PART, CL, NH>(s32, M.in0, M.nh, 0.0f, x + v * 1e-30f, y, z);
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) Y[0] = (float)(t1 - t0) / (float)reps;
@@ -68,13 +71,13 @@ __global__ __launch_bounds__(64) void k_mlp_latency_lp(MlpArgs M, const float *_
     Y[1 + lane] = PART == 0 ? v[0] + v[1] : PART >= 2 ? v[0] : __uint_as_float(kk[0][0][0] ^ kk[3][1][3]);
 }
 
-template <int PART>
+template <int PART, bool CL = false, int NH = 0>
 static void launch_lat(const MlpArgs &M, const float *X, float *Y, int reps, int nt, hipStream_t st) {
     const int sm = M.pk_bytes;
-    if (nt <= 1) hipLaunchKernelGGL((k_mlp_latency<1, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 2) hipLaunchKernelGGL((k_mlp_latency<2, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else if (nt == 3) hipLaunchKernelGGL((k_mlp_latency<3, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
-    else hipLaunchKernelGGL((k_mlp_latency<4, PART>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    if (nt <= 1) hipLaunchKernelGGL((k_mlp_latency<1, PART, CL, NH>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 2) hipLaunchKernelGGL((k_mlp_latency<2, PART, CL, NH>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else if (nt == 3) hipLaunchKernelGGL((k_mlp_latency<3, PART, CL, NH>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
+    else hipLaunchKernelGGL((k_mlp_latency<4, PART, CL, NH>), dim3(1), dim3(64), sm, st, M, X, Y, reps);
 }
 
 hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float *Y, int reps, int nt, int part,
@@ -84,7 +87,7 @@ hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float 
         const int sm = M.lp_bytes + M.lpf_bytes;
         auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(1), dim3(64), sm, st, M, X, Y, reps); };
         // nt <= 2: the tracer's 64-point form on nt 32-point tiles; else k_mlp16's 128 points
-        const int pt = part ? 1 : nt == 1 ? 3 : nt == 2 ? 2 : 0;
+        const int pt = (part & 1) ? 1 : nt == 1 ? 3 : nt == 2 ? 2 : 0;
         if (prec == NR_PRECISION_BF16) {
             if (pt == 0) go(k_mlp_latency_lp<NR_PRECISION_BF16, 0>);
             else if (pt == 1) go(k_mlp_latency_lp<NR_PRECISION_BF16, 1>);
@@ -98,8 +101,19 @@ hipError_t launch_mlp_latency(const MlpArgs &M, int prec, const float *X, float 
         }
         return hipGetLastError();
     }
-    if (part) launch_lat<1>(M, X, Y, reps, nt, st);
-    else launch_lat<0>(M, X, Y, reps, nt, st);
+    // part bit 0: no final layer; bit 1: the clamped form (needs the scaled pack); bit 2: unrolled
+    // for 7 hidden layers (needs nh == 7)
+    if (((part & 2) && !M.f32_clamp) || ((part & 4) && M.nh != 7)) return hipErrorInvalidValue;
+    switch (part & 7) {
+        case 0: launch_lat<0>(M, X, Y, reps, nt, st); break;
+        case 1: launch_lat<1>(M, X, Y, reps, nt, st); break;
+        case 2: launch_lat<0, true>(M, X, Y, reps, nt, st); break;
+        case 3: launch_lat<1, true>(M, X, Y, reps, nt, st); break;
+        case 4: launch_lat<0, false, 7>(M, X, Y, reps, nt, st); break;
+        case 5: launch_lat<1, false, 7>(M, X, Y, reps, nt, st); break;
+        case 6: launch_lat<0, true, 7>(M, X, Y, reps, nt, st); break;
+        default: launch_lat<1, true, 7>(M, X, Y, reps, nt, st); break;
+    }
     return hipGetLastError();
 }
 

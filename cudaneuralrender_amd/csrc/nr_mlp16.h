@@ -59,6 +59,54 @@ __device__ __forceinline__ float from_prev_group(float v, int q) {
     return __uint_as_float(pl16(t, t, 0));                 // [v2 v2 v2 v2]
 }
 
+// LDS byte address of a pointer into shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// The 7 hidden layers of the clamped fp32 MLP on NT <= 2 tiles as the generated stream
+// (nr_mlp16_asm.h NR_F32_HID7_NT*, tools/gen_mlp_asm.py build_f32): the loop below's instructions and
+// operands, software-pipelined -- the next layer's weights requested during this one, the ReLU of
+// row tile 1 deferred past the next layer's k-steps 0-3 -- for the latency of a wave with few rays
+// (the single frame's tail).  a: in = layer 0's ReLU'd outputs, out = the last
+// hidden layer's; the values of the loop, bit for bit.  Measured (profiles/r6_f32_stream.txt): a lone
+// wave's MLP 5,396 -> 4,756 cycles on one tile, 9,628 -> 8,876 on two; but in the fp32 tracers
+// (NR_F32_STREAM=1: one-tile waves take it) the single frame moved by -0.4 % and the batched
+// headline lost 2-3 % (the pinned registers raise the kernel's allocation, 113 -> 120 VGPRs), so
+// the tracers keep the loop and the stream is the latency diagnostic's form (nr_diag.hip part 6).
+#ifndef NR_F32_STREAM
+#define NR_F32_STREAM 0
+#endif
+template <int NT>
+__device__ __forceinline__ void f32_hidden7_stream(const float *s, float (&a)[NT][8]) {
+    typedef float f32x8 __attribute__((ext_vector_type(8)));
+    const int lane = lane_id();
+    const uint32_t va = lds_addr(s + PK_HID) + 16u * (uint32_t)lane;
+    const uint32_t vb = lds_addr(s + PK_HID + 1024) + 32u * (uint32_t)(lane >> 4);
+    f32x8 k[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        k[t] = f32x8{a[t][0], a[t][1], a[t][2], a[t][3], a[t][4], a[t][5], a[t][6], a[t][7]};
+    f32x16 c0, c1, w0, w1, b0;
+    if constexpr (NT == 1) {
+        asm volatile(NR_F32_HID7_NT1
+                     : "+{v[16:23]}"(k[0]), "=&{v[0:15]}"(c0), "=&{v[24:39]}"(w0), "=&{v[40:55]}"(w1),
+                       "=&{v[56:71]}"(b0)
+                     : [va] "v"(va), [vb] "v"(vb)
+                     : "memory");
+    } else {
+        asm volatile(NR_F32_HID7_NT2
+                     : "+{v[32:39]}"(k[0]), "+{v[40:47]}"(k[NT - 1]), "=&{v[0:15]}"(c0), "=&{v[16:31]}"(c1),
+                       "=&{v[48:63]}"(w0), "=&{v[64:79]}"(w1), "=&{v[80:95]}"(b0)
+                     : [va] "v"(va), [vb] "v"(vb)
+                     : "memory");
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[t][i] = k[t][i];
+}
+
 // FP32 MLP on NT active tiles (tiles 0..NT-1; the caller keeps live points there).
 // PART != 0 only in the latency diagnostic (nr_diag.hip): stop after the hidden layers.
 // CL: bias add and ReLU as one v_add_f32 / v_fma_f32 with the clamp bit (clamp to [0, 1]),
@@ -66,9 +114,11 @@ __device__ __forceinline__ float from_prev_group(float v, int q) {
 // where every activation is at most 1/2: bit-equal to fmaxf(v, 0) (NaN and -0 aside, which
 // the chains of the next layer map to the same values).  Every VALU instruction costs f32
 // matrix time on gfx950 (profiles/r1_mfma_peak.txt), and this halves the activation VALU.
-template <int NT, int PART = 0, bool CL = false>
-__device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh, float fr, float x,
+// NH == 7 (the caller checks nh == 7): the stream below for NT <= 2 with the clamped ReLU
+template <int NT, int PART = 0, bool CL = false, int NH = 0>
+__device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int in0, int nh_rt, float fr, float x,
                                                float y, float z) {
+    const int nh = NH > 0 ? NH : nh_rt;
     auto relu = [](float v) { return CL ? __builtin_amdgcn_fmed3f(v, 0.0f, 1.0f) : fmaxf(v, 0.0f); };
     // fr: this lane's 4th input (the frame number when rendering; used iff in0 == 4)
     const int lane = lane_id(), g = lane >> 4;
@@ -111,7 +161,9 @@ __device__ __forceinline__ float mlp16_fp32_nt(const float *__restrict__ s, int 
                 for (int r = 0; r < 4; ++r) a[t][4 * mt + r] = relu(__builtin_fmaf(c[t][mt][r], s0, bias[4 * mt + r]));
     }
     // hidden 32x32 layers: 8 k-steps x 2 row tiles of v_mfma_f32_16x16x4_f32 per point tile
-    for (int jl = 0; jl < nh; ++jl) {
+    constexpr bool STREAM = NT <= 2 && CL && NH == 7 && PART == 0;
+    if constexpr (STREAM) f32_hidden7_stream<NT>(s, a);
+    for (int jl = 0; jl < (STREAM ? 0 : nh); ++jl) {
         const float *L = s + PK_HID + jl * PK_HID_STRIDE;
         float4 wq[4];
 #pragma unroll
@@ -211,21 +263,28 @@ __device__ __forceinline__ bool inputs_in_bound_f32(float x, float y, float z, f
 // cl (wave-uniform): the pack is scaled (MlpArgs::f32_clamp) and the inputs are within the
 // bound -- the clamped form on the active tiles; otherwise (never on the bundled networks'
 // rays) the add + max form on all four tiles, which keeps one extra copy of the MLP code
-// in the kernels instead of four
+// in the kernels instead of four.  ST: one tile of a 7-hidden-layer network on the stream
+// (f32_hidden7_stream; the fp32 tracers' march -- its pinned registers cost the other callers'
+// register allocations more than its latency gains them)
+template <bool ST = false>
 __device__ __forceinline__ float mlp16_fp32(const float *__restrict__ s, int in0, int nh, float fr, float x, float y,
                                             float z, uint32_t tmask, bool cl) {
     const int nt = 32 - __clz((int)tmask);  // highest active tile + 1
     if (cl) {
         if (nt >= 4) return mlp16_fp32_nt<4, 0, true>(s, in0, nh, fr, x, y, z);
         if (nt == 3) return mlp16_fp32_nt<3, 0, true>(s, in0, nh, fr, x, y, z);
+        // one or two tiles (a wave with few rays: the tail): the stream for 7 hidden layers
+        if (nt == 2) return mlp16_fp32_nt<2, 0, true>(s, in0, nh, fr, x, y, z);
+        if (ST && NR_F32_STREAM && nh == 7) return mlp16_fp32_nt<1, 0, true, 7>(s, in0, nh, fr, x, y, z);
         if (nt == 2) return mlp16_fp32_nt<2, 0, true>(s, in0, nh, fr, x, y, z);
         return mlp16_fp32_nt<1, 0, true>(s, in0, nh, fr, x, y, z);
     }
     return mlp16_fp32_nt<4>(s, in0, nh, fr, x, y, z);
 }
+template <bool ST = false>
 __device__ __forceinline__ float mlp16_fp32(const MlpArgs &M, const float *s, float fr, float x, float y, float z,
                                             uint32_t tmask) {
-    return mlp16_fp32(s, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
+    return mlp16_fp32<ST>(s, M.in0, M.nh, fr, x, y, z, tmask, M.f32_clamp && inputs_in_bound_f32(x, y, z, fr));
 }
 
 // bf16 / fp16: the whole MLP on 32-point tiles, v_mfma_f32_32x32x16_{bf16,f16} (nr_internal.h
@@ -464,10 +523,6 @@ __device__ __forceinline__ float hi16f(uint32_t p) {
 // The pipelined stream (nr_mlp16_asm.h, tools/gen_mlp_asm.py) of the 7-hidden-layer networks runs
 // k_mlp16's 128-point form (MlpArgs::lp_stream; nr_set_debug bit 11 selects the builtin form).
 
-// LDS byte address of a pointer into shared memory
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
 
 // CL: ReLU by the conversion's clamp (bf16 with the clamped pack, inputs within
 // LP_INPUT_BOUND -- the caller checks); otherwise cvt + v_pk_max_i16 (any pack, any input).
@@ -977,7 +1032,7 @@ __device__ __forceinline__ float mlp16(const MlpArgs &M, const float *s32, const
     if (prec == NR_PRECISION_BF16) return mlp16_lowp<NR_PRECISION_BF16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP16) return mlp16_lowp<NR_PRECISION_FP16>(slp, sfl, M.in0, M.nh, fr, x, y, z, tmask, cl);
     if (prec == NR_PRECISION_FP32X3) return mlp16_x3(M, s32, slp, sfl, fr, x, y, z, tmask, M.lp_clamp != 0);
-    return mlp16_fp32(M, s32, fr, x, y, z, tmask);
+    return mlp16_fp32<true>(M, s32, fr, x, y, z, tmask);
 }
 
 // wave-uniform: every lane's inputs are within LP_INPUT_BOUND (NaN is not)

@@ -258,7 +258,8 @@ int nr_set_schedule(nr_ctx *ctx, int schedule);
  * MLP latency probe: nr_mlp_forward(X >= 64 points, Y >= 65 floats, n = repetitions, on
  * the device) runs one wave of ceil(wave_rays / 16) tiles n times back to back and
  * writes the shader cycles per evaluation to Y[0]; bit 7 times it without the final
- * layer.  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
+ * layer; for fp32, bit 13 in the clamped-ReLU form the tracers run (scaled pack) and bit 14 with
+ * the hidden layers unrolled for 7 (the network must have 7).  Bit 8 = NR_SCHED_LAYERED issues its launches one by one instead of replaying
  * the captured hipGraph (for profilers that do not follow graph launches).  Bit 9 = the plain ReLU
  * forms on the scaled packs: bf16 by v_pk_max_i16 instead of the conversion's clamp bit,
  * fp32 by add + max instead of v_add_f32 with the clamp bit (the same values: parity and

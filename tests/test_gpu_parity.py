@@ -329,10 +329,10 @@ def test_schedule_knobs_same_pixels(rend, nets, chrome, W, H):
             assert np.array_equal(img, ref), (spread, bpc)
             for k in ("ray_steps", "shade_evals", "rays_hit", "rays_shaded", "iterations"):
                 assert st[k] == sref[k], (k, spread, bpc)
-        # rays per wave: explicit 64 / 32 and automatic (0: 32 for an fp32 launch of at most 2x
+        # rays per wave: explicit 64 / 32 / 16 (one tile: the fp32 stream, f32_hidden7_stream) and automatic (0: 32 for an fp32 launch of at most 2x
         # its waves' slots, this frame on 8 shards)
         rend.set_pixel_spread(-1).set_occupancy(0)
-        for rays in (64, 32, 0):
+        for rays in (64, 32, 16, 0):
             rend.set_wave_rays(rays)
             img, st = rend.render(W, H, 128)
             assert np.array_equal(img, ref) and st["ray_steps"] == sref["ray_steps"], rays

@@ -67,9 +67,10 @@ PERM_RAW = 2
 
 
 class Stream:
-    def __init__(self, nt=4):
+    def __init__(self, nt=4, raw=None):
         self.ins = []   # (text, kind, reads, writes, states)
         self.nt = nt
+        self.raw = MFMA_VALU_RAW if raw is None else raw   # MFMA -> VALU read distance of its MFMAs
 
     def add(self, text, kind, reads=(), writes=(), states=1):
         self.ins.append((text, kind, tuple(reads), tuple(writes), states))
@@ -90,7 +91,7 @@ class Stream:
                 break
             if k == "mfma" and kind != "mfma":
                 if any(r in wr for r in regs) or any(r in wr for r in writes):
-                    need = max(need, MFMA_VALU_RAW - dist)
+                    need = max(need, self.raw - dist)
                 for role, r in rd:
                     if r in writes:
                         need = max(need, (SRCC_WAR if role == "C" else SRCAB_WAR) - dist)
@@ -339,6 +340,95 @@ def build_s16(prec, clamp):
     return st
 
 
+# v_mfma_f32_16x16x4_f32 -> VALU read: hipcc pads 10 wait states on gfx950 (its minimum over the
+# fp32 tracer's listing); two more here as margin
+F32_MFMA_VALU_RAW = 12
+
+
+def build_f32(nt):
+    """The fp32 MLP's 7 hidden layers (clamped ReLU, the scaled pack: nr_mlp16.h mlp16_fp32_nt<NT, 0,
+    true>) for NT <= 2 16-point tiles as one stream (round 6, VERDICT r5 item 4: the latency of a
+    wave with few rays, the single frame's tail).  The compiled form issues a layer's 16 NT MFMAs,
+    then waits for the last, then converts all 8 NT accumulators and only then requests the next
+    layer's weights, so every layer boundary costs an MFMA drain, the ReLUs and an LDS round trip
+    with the matrix pipe idle.  Here (the same instructions and operands, so the same values):
+      * the next layer's weights and bias are read into the other of two register buffers during
+        this layer (its first MFMAs / after its deferred ReLUs);
+      * the accumulators alternate between two buffers by layer, so that the ReLU of row tile 1
+        (units 16-31 = k-steps 4-7 of the next layer) is deferred until the next layer's k-steps
+        0-3 have issued: at a boundary only row tile 0's four ReLUs stand between the last MFMA
+        and the next one.
+    MFMA(l, st, mt, t): acc(l % 2, t, mt) (+)= W[2 st + mt] x act(t, st), k-step st = 0 from 0 --
+    the k-ascending fmaf chain of every output, as the compiled form.  Registers: accumulators
+    v[0 : 16 NT) (buffer b, tile t, row tile mt at 8 NT b + 8 t + 4 mt), activations v[16 NT : 24 NT)
+    (tile t, k-step st at 16 NT + 8 t + st: in = layer 0's ReLU'd outputs, out = the last hidden
+    layer's), weights 2 x 16 from v[24 NT], biases 2 x 8 after them.  %[va] = LDS byte address of
+    the pack's hidden layers + 16 lane, %[vb] = of their biases + 32 (lane >> 4)."""
+    st = Stream(nt, raw=F32_MFMA_VALU_RAW)
+    ACC = lambda b, t, mt: 8 * nt * b + 8 * t + 4 * mt
+    ACT = lambda t, s: 16 * nt + 8 * t + s
+    W = lambda b: 24 * nt + 16 * b
+    BIAS = lambda b: 24 * nt + 32 + 8 * b
+    STRIDE = 4 * (1024 + 32)   # bytes per hidden layer in the pack (nr_internal.h PK_HID_STRIDE)
+
+    def load(dst, addr, off):
+        o = f" offset:{off}" if off else ""
+        st.pad("lds", (), list(rng(dst, 4)))
+        st.add(f"ds_read_b128 v[{dst}:{dst + 3}], %[{addr}]{o}", "lds", writes=list(rng(dst, 4)))
+
+    def w_loads(b, j):
+        for q in range(4):
+            load(W(b) + 4 * q, "va", j * STRIDE + 1024 * q)
+
+    def b_loads(b, j):
+        load(BIAS(b), "vb", j * STRIDE)
+        load(BIAS(b) + 4, "vb", j * STRIDE + 16)
+
+    def mfma(l, s, mt, t):
+        b = l % 2
+        d, a, bb = ACC(b, t, mt), W(b) + 2 * s + mt, ACT(t, s)
+        reads = [("A", a), ("B", bb)] + ([("C", r) for r in rng(d, 4)] if s else [])
+        st.pad("mfma", reads, list(rng(d, 4)))
+        c = f"v[{d}:{d + 3}]" if s else "0"
+        st.add(f"v_mfma_f32_16x16x4_f32 v[{d}:{d + 3}], v{a}, v{bb}, {c}", "mfma", reads=reads, writes=list(rng(d, 4)))
+
+    def relu(l, mt):
+        b = l % 2
+        for t in range(nt):
+            for r in range(4):
+                src, bias, dst = ACC(b, t, mt) + r, BIAS(b) + 4 * mt + r, ACT(t, 4 * mt + r)
+                st.pad("valu", [src, bias], [dst])
+                st.add(f"v_add_f32_e64 v{dst}, v{src}, v{bias} clamp", "valu", reads=[src, bias], writes=[dst])
+
+    wait = lambda: st.add("s_waitcnt lgkmcnt(0)", "wait")
+    w_loads(0, 0)
+    b_loads(0, 0)
+    for l in range(NH):
+        wait()
+        nxt = l < NH - 1
+        for s in range(8):
+            if s == 4:
+                if l > 0:
+                    relu(l - 1, 1)              # the previous layer's row tile 1 -> k-steps 4-7
+                if nxt:
+                    b_loads((l + 1) % 2, l + 1)  # (its bias buffer's last reader was that ReLU)
+            for mt in range(2):
+                for t in range(nt):
+                    mfma(l, s, mt, t)
+            if s == 0 and nxt:
+                w_loads((l + 1) % 2, l + 1)      # (the other buffer's readers: layer l - 1's MFMAs)
+        relu(l, 0)                              # row tile 0 -> the next layer's k-steps 0-3
+    relu(NH - 1, 1)
+    dist, need = 0, 0
+    for text, k, rd, wr, states in reversed(st.ins):
+        if k == "mfma":
+            need = max(need, max(SRCC_WAR if role == "C" else SRCAB_WAR for role, _ in rd) - dist)
+        dist += states
+    st.nop(need)
+    check(st, inputs=[ACT(t, s) for t in range(nt) for s in range(8)])
+    return st
+
+
 def check(st, inputs=None):
     """Verifies every hazard of the stream (raises on the first violation).  inputs: the registers
     the compiler's VALU wrote just before the stream (default: the k-step-0 B operands)."""
@@ -365,7 +455,7 @@ def check(st, inputs=None):
             if r in last_w:
                 wi, wk = last_w[r]
                 dist = pos[i] - (pos[wi] + st.ins[wi][4]) if wi >= 0 else pos[i]   # states in between
-                if wk == "mfma" and kind != "mfma" and dist < MFMA_VALU_RAW:
+                if wk == "mfma" and kind != "mfma" and dist < st.raw:
                     raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after MFMA {wi}")
                 if wk in ("valu", "perm") and kind == "mfma" and dist < VALU_MFMA_RAW:
                     raise AssertionError(f"{i}: {text}: reads v{r} {dist} states after VALU {wi}")
@@ -384,7 +474,7 @@ def check(st, inputs=None):
                     raise AssertionError(f"{i}: {text}: writes v{r} {dist} states after MFMA {ri} read it as {role}")
             if r in last_w and last_w[r][1] == "mfma" and kind != "mfma":
                 wi = last_w[r][0]
-                if pos[i] - (pos[wi] + st.ins[wi][4]) < MFMA_VALU_RAW:
+                if pos[i] - (pos[wi] + st.ins[wi][4]) < st.raw:
                     raise AssertionError(f"{i}: {text}: overwrites v{r} too soon after MFMA {wi}")
         for r in writes:
             last_w[r] = (i, kind)
@@ -398,7 +488,7 @@ def check(st, inputs=None):
         raise AssertionError("LDS loads left outstanding at the end of the stream")
     # nothing in flight at the exit: the compiler may read or overwrite any register right after
     for r, (wi, wk) in last_w.items():
-        if wk == "mfma" and p - (pos[wi] + st.ins[wi][4]) < MFMA_VALU_RAW:
+        if wk == "mfma" and p - (pos[wi] + st.ins[wi][4]) < st.raw:
             raise AssertionError(f"v{r}: MFMA {wi} may still be writing it when the stream ends")
     for r, lst in last_r.items():
         for (ri, role) in lst:
@@ -453,6 +543,22 @@ def main():
         parts.append(f"// {prec}, 8 x 16-point tiles, {'clamped' if clamp else 'max'} ReLU: {len(st.ins)} instructions, "
                      f"{nm} MFMA, {nv} VALU, {nn} s_nop states")
         parts.append(f"#define {name} \\")
+        parts.append(emit(st).replace("\n", " \\\n") + "")
+        parts.append("")
+    parts += [
+        "// The fp32 MLP's 7 hidden layers, clamped ReLU, for NT = 1, 2 16-point tiles (build_f32): the",
+        "// compiled form's instructions and operands, software-pipelined; registers v[0 : 24 NT + 48)",
+        "// (accumulators v[0 : 16 NT), activations v[16 NT : 24 NT) in and out, weights and biases after);",
+        "// %[va] = LDS byte address of the pack's hidden layers + 16 lane, %[vb] = of their biases + 32 (lane >> 4).",
+        "",
+    ]
+    for nt in (1, 2):
+        st = build_f32(nt)
+        nm = sum(1 for x in st.ins if x[1] == "mfma")
+        nv = sum(1 for x in st.ins if x[1] == "valu")
+        nn = sum(x[4] for x in st.ins if x[1] == "nop")
+        parts.append(f"// fp32, {nt} tile(s): {len(st.ins)} instructions, {nm} MFMA, {nv} VALU, {nn} s_nop states")
+        parts.append(f"#define NR_F32_HID7_NT{nt} \\")
         parts.append(emit(st).replace("\n", " \\\n") + "")
         parts.append("")
     text = "\n".join(parts) + "\n"
