@@ -85,6 +85,31 @@ def test_group_copy_multi_rank_on_one_gpu(chrome, prec, n):
             r.close()
 
 
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_group_copy_over_distinct_gpus(chrome, asynchronous):
+    """NR_GROUP_COPY with its contexts on different GPUs (the COPY-mode events are
+    created on GPU 0 and waited on by every rank's streams): 2 ranks on GPUs 0 and 1, host and
+    device outputs, synchronous and NR_GROUP_ASYNC.  Needs 2 GPUs (skipped on a one-GPU box)."""
+    if NGPU < 2:
+        pytest.skip(f"2 GPUs needed, {NGPU} visible")
+    cams = [(*nr.camera(5.0 * i, 12.0 + 31 * i, 2.0), i) for i in range(3)]
+    rs = [_setup(nr.Renderer(d), "fp32", chrome) for d in (0, 1)]
+    try:
+        refs = _refs(rs[0], cams, 200, 131, 128)
+        with nr.Group(rs, copy=True, asynchronous=asynchronous) as g:
+            imgs, _ = g.render_batch(200, 131, cams, 128, band=1)
+            assert all(np.array_equal(a, b[0]) for a, b in zip(imgs, refs))
+            outs = torch.zeros(len(cams), 131 * 200, dtype=torch.int32, device="cuda:0")
+            g.render_batch_device([o.data_ptr() for o in outs], 200, 131, cams, 128, band=8)
+            g.synchronize()
+            torch.cuda.synchronize()
+            for o, b in zip(outs, refs):
+                assert np.array_equal(o.cpu().numpy().view(np.uint32).reshape(131, 200), b[0])
+    finally:
+        for r in rs:
+            r.close()
+
+
 def test_group_async_calls_overlap_and_stay_exact(chrome):
     """NR_GROUP_ASYNC: five calls back to back (set k & 1 reused every other call, its render
     waiting on the transfer of the call before last), then one synchronize: every frame of every
