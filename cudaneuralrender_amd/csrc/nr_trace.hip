@@ -181,7 +181,10 @@ __device__ __forceinline__ void set_priority(int prio) {
 // whole loop.  The pointer is made opaque per use, so the loads cannot be
 // hoisted out of the loop.  The struct mirrors the kernarg layout of k_trace(A, M, T): each
 // argument at its natural alignment, in order (the code object metadata, llvm-readelf --notes:
-// by_value arguments at offsets 0, 200 and 304; every GPU parity test reads through it).
+// by_value arguments at offsets 0, 200 and 304; tests/test_lib_cpu.py
+// test_trace_kernarg_layout_matches_trace_kargs checks every instance of the built library, and every
+// GPU parity test reads through it).  (Taking the parameters' addresses instead makes the compiler
+// copy them to scratch: 368 bytes per lane.)
 // (SGPRs spilled to VGPR lanes: the bf16 batched tracer with fp32x3 normals 124 -> 59, its endgame
 // instance 151 -> 51, the fp32 batched tracer 85 -> 8.)
 #ifndef NR_ARG_RELOAD

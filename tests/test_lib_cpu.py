@@ -301,6 +301,38 @@ def test_batched_fp32_tracer_has_no_scratch(tmp_path):
     assert r["private_segment_fixed_size"] <= 16 and r["vgpr_count"] <= 168, r
 
 
+def test_trace_kernarg_layout_matches_trace_kargs(tmp_path):
+    """Round 6 (nr_trace.hip fresh_kargs): k_trace re-reads its arguments through a TraceKargs
+    {RenderArgs A; MlpArgs M; TraceArgs T;} view of the kernarg segment, which holds iff the code
+    object puts the three by-value arguments where that struct's layout does: back to back, each
+    at the next 8-byte boundary (every one holds pointers / doubles), from offset 0.  Checked
+    here on every k_trace instance's metadata in the built library."""
+    import shutil
+    import subprocess
+    readelf, objdump = "/opt/rocm/lib/llvm/bin/llvm-readelf", "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not (os.path.exists(readelf) and os.path.exists(objdump)):
+        pytest.skip("llvm-readelf / llvm-objdump not available")
+    so = tmp_path / "libnr.so"
+    shutil.copy(_lib.LIB_PATH, so)
+    subprocess.run([objdump, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    seen = 0
+    for p in sorted(p for p in tmp_path.iterdir() if "amdgcn" in p.name and "gfx950" in p.name):
+        notes = subprocess.run([readelf, "--notes", str(p)], check=True, capture_output=True, text=True).stdout
+        for kern in notes.split("  - .agpr_count:")[1:]:
+            m = re.search(r"\.name:\s+(\S+)", kern)
+            if not m or "k_trace" not in m.group(1):
+                continue
+            args = re.findall(r"\.offset:\s+(\d+)\s+\.size:\s+(\d+)\s+\.value_kind:\s+(\w+)", kern)
+            byval = [(int(o), int(s)) for o, s, k in args if k == "by_value"]
+            assert len(byval) == 3, (m.group(1), byval)
+            off = 0
+            for o, s in byval:
+                assert o == off, (m.group(1), byval)
+                off = (o + s + 7) // 8 * 8
+            seen += 1
+    assert seen >= 8, seen
+
+
 def test_batch_frames_per_launch_fits_the_queue_counters():
     """nr_render_batch caps the frames of one launch so that the busiest pixel-queue shard's
     positions (plus the waves' over-reservation) stay below 2^32 (16384^2 x 16
