@@ -169,7 +169,7 @@ def live_traffic(frames, precision, size, max_steps):
     prof = shutil.which("rocprofv3")
     if prof is None or "ROCPROF_OUTPUT_PATH" in os.environ:   # absent, or this run is itself profiled
         return None
-    kname = "k_trace<0, false, false, true, false, false>"
+    kname = "k_trace<0, false, false, true, false, false"  # (a prefix: later template arguments follow)
     tmp = tempfile.mkdtemp(prefix="nr_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     vals = {}

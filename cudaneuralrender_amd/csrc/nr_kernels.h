@@ -17,6 +17,8 @@
 #ifndef NR_EG_WAVES
 #define NR_EG_WAVES 12
 #endif
+// LDS per CU on gfx950 (MI355X_MICROARCH.md): one workgroup's static + dynamic LDS must fit
+constexpr int NR_LDS_PER_CU = 160 * 1024;
 
 namespace nr {
 

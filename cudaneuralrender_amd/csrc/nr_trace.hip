@@ -230,8 +230,12 @@ __device__ __forceinline__ const TraceKargs *fresh_kargs() {
 // spills cost C3 +25 %, C5 +40-55 %; a pass per 64 queued rays instead of 32: C5 batch +5-10 %;
 // profiles/r5_ab_eg.txt)
 // (NR_TRACE_BPC_EG: nr_kernels.h, where the host side caps the grid with it)
-template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false>
-__global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
+// EGL (EG only): the NR_EG_WAVES-wave workgroup with the fp32x3 pack in LDS; false = 4-wave
+// workgroups reading it from global memory, for networks whose two packs do not fit the CU's LDS
+// beside the 12 waves' queues (more than 9 hidden layers; launch_trace_k chooses)
+template <int PREC, bool PROBE, bool STAMPS = false, bool BATCH = false, bool NX3 = false, bool EG = false,
+          bool EGL = true>
+__global__ __launch_bounds__(EG && EGL ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
                                   : PREC == NR_PRECISION_FP32X3 ? NR_TRACE_BPC_X3
                                   : PREC != NR_PRECISION_FP32 ? NR_TRACE_BPC_LOWP
                                   : BATCH ? NR_TRACE_BPC_WIDE : NR_TRACE_BPC) void k_trace(RenderArgs A, MlpArgs M, TraceArgs T) {
@@ -257,8 +261,8 @@ __global__ __launch_bounds__(EG ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_BPC_EG
     }
     // waves per workgroup: 4, or NR_EG_WAVES for the endgame instances, which then hold the fp32x3
     // pack in LDS (X3L) for their fine passes and normals
-    constexpr int NW = EG ? NR_EG_WAVES : 4;
-    constexpr bool X3L = EG && NR_EG_WAVES > 4;
+    constexpr int NW = EG && EGL ? NR_EG_WAVES : 4;
+    constexpr bool X3L = EG && EGL && NR_EG_WAVES > 4;
     const uint16_t *x3l = M.x3lp;
     const float *x3f = M.x3fl;
     if constexpr (X3L) stage_x3<PREC>(M, T.x3lp_bytes, T.x3fl_bytes, x3l, x3f);
@@ -1178,12 +1182,24 @@ static hipError_t launch_trace_k(const RenderArgs &A, const MlpArgs &M, const Tr
         if constexpr (!STAMPS) {
             if (M.x3n && T.eg_tau > 0.0f) {
                 // the grid is at most NR_TRACE_BPC_EG 4-wave workgroups per CU (nr_api.hip trace_bpc):
-                // as NR_EG_WAVES-wave workgroups, one per CU, with the fp32x3 pack in their LDS
+                // as NR_EG_WAVES-wave workgroups, one per CU, with the fp32x3 pack in their LDS --
+                // when the two packs fit beside the instance's static LDS (networks of up to 9 hidden
+                // layers), else as round 5's 4-wave workgroups reading the pack from global memory
                 constexpr int G = NR_EG_WAVES / 4;
-                const int g = std::max(1, (grid + G - 1) / G);
-                const int smx = NR_EG_WAVES > 4 ? smem16_bytes(M, PREC, true, T.x3lp_bytes + T.x3fl_bytes) : sm;
-                hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true>), dim3(g), dim3(64 * NR_EG_WAVES), smx, st,
-                                   A, M, T);
+                const int smx = smem16_bytes(M, PREC, true, T.x3lp_bytes + T.x3fl_bytes);
+                static const int static_lds = [] {
+                    hipFuncAttributes fa{};
+                    const void *k = reinterpret_cast<const void *>(&k_trace<PREC, PROBE, STAMPS, BATCH, true, true, true>);
+                    return hipFuncGetAttributes(&fa, k) == hipSuccess ? (int)fa.sharedSizeBytes : (1 << 30);
+                }();
+                if (NR_EG_WAVES > 4 && static_lds + smx <= NR_LDS_PER_CU) {
+                    const int g = std::max(1, (grid + G - 1) / G);
+                    hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true, true>), dim3(g), dim3(64 * NR_EG_WAVES),
+                                       smx, st, A, M, T);
+                } else {
+                    hipLaunchKernelGGL((k_trace<PREC, PROBE, STAMPS, BATCH, true, true, false>), dim3(grid), dim3(256), sm,
+                                       st, A, M, T);
+                }
                 return hipGetLastError();
             }
         }

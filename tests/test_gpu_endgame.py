@@ -160,6 +160,29 @@ def test_endgame_four_input_network_frame_bound():
     assert any((i != 0).any() for i in imgs)
 
 
+@pytest.mark.parametrize("extra", [2, 5])
+def test_endgame_deep_networks(chrome, extra):
+    """Deeper fused networks (plane_1 with `extra` identity hidden layers inserted: 9 and 12 hidden
+    layers, the same function): the endgame's 12-wave workgroups hold both packs in LDS only up to
+    ~9 hidden layers; deeper networks take the 4-wave instances that read the fp32x3 pack from
+    global memory (nr_trace.hip launch_trace_k).  Both bit-exact with the oracle's restatement."""
+    dims, K, B = nr.read_keras_h5(nr.geometry_path("plane_1"))
+    K, B = list(K), list(B)
+    for _ in range(extra):
+        K.insert(4, np.eye(32, dtype=np.float32))
+        B.insert(4, np.zeros(32, dtype=np.float32))
+    dims = [3] + [32] * (len(K) - 1) + [1]
+    net = _oracle(dims, K, B)
+    iv, nm = nr.camera(-15.0, 30.0, 2.0)
+    with nr.Renderer(0) as r:
+        r.load_mlp(dims, K, B).set_precision("bf16")
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        img, st = r.render(112, 96, 96)
+    ref, rst = net.render(112, 96, iv, nm, color_type=1, matcap=chrome, max_steps=96, nthreads=16, precision=1,
+                          endgame=nr.NR_ENDGAME_DEFAULT)
+    _check(img, st, ref, rst)
+
+
 def test_endgame_off_for_fp32_normals(chrome):
     """Bit 15 (fp32 normals) marches in pure 16-bit (no fp32x3 pass), on both schedules."""
     with nr.Renderer(0) as r:

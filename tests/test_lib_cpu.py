@@ -286,7 +286,7 @@ def test_batched_fp32_tracer_has_no_scratch(tmp_path):
     the ds_bpermute addresses of the quad and lane-group shuffles; mbcnt, DPP quad_perm and
     v_permlane swaps need none.)  The stand-alone MLP's fp32 and bf16 instances stay spill-free."""
     res = kernel_resources(_lib.LIB_PATH, tmp_path)
-    want = {"_ZN2nr7k_traceILi0ELb0ELb0ELb1ELb0ELb0EEEvNS_10RenderArgsENS_7MlpArgsENS_9TraceArgsE": 128,
+    want = {"_ZN2nr7k_traceILi0ELb0ELb0ELb1ELb0ELb0ELb1EEEvNS_10RenderArgsENS_7MlpArgsENS_9TraceArgsE": 128,
             "_ZN2nr7k_mlp16ILi0ELi3ELb0EEEvNS_7MlpArgsEPKfPfi": 512,
             # round 6: the 16x16x32 instances (128 pinned registers), the default for bf16 / fp16
             "_ZN2nr7k_mlp16ILi1ELi3ELb1EEEvNS_7MlpArgsEPKfPfi": 168,

@@ -11,7 +11,8 @@ import sys
 
 out = sys.argv[1]
 batch = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-kname = "k_trace<0, false, false, true, false, false>" if batch else "k_trace<0, false, false, false, false, false>"
+# (prefixes of the demangled names: later template arguments follow)
+kname = "k_trace<0, false, false, true, false, false" if batch else "k_trace<0, false, false, false, false, false"
 
 
 def per_dispatch(counter_dir, name):
