@@ -201,6 +201,16 @@ __device__ __forceinline__ const TraceKargs *fresh_kargs() {
     return (const TraceKargs *)p;
 }
 
+// The shading pass's fp32x3 normals as two one-tile passes (1, round 4: fewer live registers at the
+// shading site) or one two-tile pass (0; A/B); _EG: in the endgame instances, whose 150+ VGPRs hold
+// the two-tile pass without spilling: 1-2 % faster batched (round 6, profiles/r6_x3n_eg_ab.txt)
+#ifndef NR_X3N_ONE
+#define NR_X3N_ONE 1
+#endif
+#ifndef NR_X3N_ONE_EG
+#define NR_X3N_ONE_EG 0
+#endif
+
 // PROBE: the cost-probe pre-pass (TraceArgs::probe) -- one ray per 8x8 block, at most
 // T.take rays per wave, no pixels written; each block's bcost gets its probe ray's
 // iteration count (max_steps is the probe's cap).
@@ -636,7 +646,7 @@ __global__ __launch_bounds__(EG && EGL ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_B
             // the shading loop into registers held for the kernel's life
             int zoff_x3 = 0;
             if constexpr (NX3) asm volatile("" : "+s"(zoff_x3));
-            const float sdf = NX3 ? mlp16_x3_normal(M, S.s32, (X3L ? x3l : M.x3lp) + zoff_x3, (X3L ? x3f : M.x3fl) + zoff_x3, fr_of(sfr), pq.x, pq.y,
+            const float sdf = NX3 ? mlp16_x3_normal<(EG ? NR_X3N_ONE_EG : NR_X3N_ONE) != 0>(M, S.s32, (X3L ? x3l : M.x3lp) + zoff_x3, (X3L ? x3f : M.x3fl) + zoff_x3, fr_of(sfr), pq.x, pq.y,
                                                     pq.z, smask)
                                   : mlp16_fp32(M, S.s32, fr_of(sfr), pq.x, pq.y, pq.z, smask);
             const F3 cq = mul3s(tp, scene_sdf(pq, sdf, A.scene, zoff_of(sfr)));
