@@ -402,12 +402,15 @@ int default_bpc(const nr_ctx *c, size_t total, int nframes) {
     return total < 2 * M ? 3 : 4;
 }
 
-// Workgroups per CU of a persistent launch: nr_set_occupancy's value or default_bpc's, at most
-// NR_TRACE_BPC_EG for the endgame's instances (eg: a bf16/fp16 launch with T.eg_tau > 0; the
-// diagnostic stamps and probe instances march without the endgame, launch_trace_k)
+// Workgroups per CU of a persistent launch: nr_set_occupancy's value or default_bpc's; for the
+// endgame's instances (eg: a bf16/fp16 launch with T.eg_tau > 0; the diagnostic stamps and probe
+// instances march without the endgame, launch_trace_k) NR_TRACE_BPC_EG 4-wave workgroups' worth:
+// with NR_EG_WAVES > 4 exactly that -- launch_trace_k runs them as one NR_EG_WAVES-wave workgroup
+// per CU, and fewer would leave CUs idle -- else at most that
 int trace_bpc(const nr_ctx *c, size_t total, int nframes, bool eg) {
     const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_bpc(c, total, nframes);
-    return eg ? std::min(bpc, NR_TRACE_BPC_EG) : bpc;
+    if (eg) return NR_EG_WAVES > 4 ? NR_TRACE_BPC_EG : std::min(bpc, NR_TRACE_BPC_EG);
+    return bpc;
 }
 
 // Rays per wave of a persistent launch (nr_set_wave_rays; 0 = automatic): an fp32 launch whose

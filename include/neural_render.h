@@ -296,7 +296,8 @@ int nr_set_endgame(nr_ctx *ctx, float tau);
  * 3x3 neighbourhood (for a moving camera, whose silhouettes shift between frames). */
 int nr_set_temporal_order(nr_ctx *ctx, int on);
 /* Persistent-schedule grid: blocks of 4 waves per CU (0 = default).  A bf16/fp16 launch with the
- * endgame on runs at most 3 per CU (its instances are built for that), whatever is set here. */
+ * endgame on runs one 12-wave workgroup per CU (3 blocks' worth, with the fp32x3 weights in its LDS;
+ * networks of more than 9 hidden layers: at most 3 blocks of 4 waves), whatever is set here. */
 int nr_set_occupancy(nr_ctx *ctx, int blocks_per_cu);
 /* Rays per wave (persistent schedule, 1-64; 0 = automatic, the default): a wave marches at
  * most this many rays at once (in lanes 0..rays-1), so 16 or 32 make every iteration one or
