@@ -183,6 +183,26 @@ def test_endgame_deep_networks(chrome, extra):
     _check(img, st, ref, rst)
 
 
+@pytest.mark.parametrize("prec", ["bf16", "fp16"])
+@pytest.mark.parametrize("tau", [0.0, nr.NR_ENDGAME_DEFAULT])
+def test_sixteen_ray_waves_bitexact(chrome, prec, tau):
+    """Waves capped at 16 rays (nr_set_wave_rays 16: every march MLP on one 32-point tile with points
+    16-31 idle, the shape of a launch's tail) bit-exact with the oracle's restatement, pure march and
+    endgame.  (Round 6 ran these waves on one 16-point tile of v_mfma_f32_16x16x32, bit-exact, and
+    removed that form again: profiles/r6_s16_tail_mlp.txt.)"""
+    net = _oracle("car_1")
+    iv, nm = nr.camera(-12.0, 40.0, 2.0)
+    with nr.Renderer(0) as r:
+        r.load_h5(nr.geometry_path("car_1")).set_precision(prec).set_endgame(tau).set_wave_rays(16)
+        r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
+        img, st = r.render(120, 104, 128)
+    ref, rst = net.render(120, 104, iv, nm, color_type=1, matcap=chrome, max_steps=128, nthreads=16,
+                          precision=PREC[prec], endgame=tau)
+    assert (ref != 0).any()
+    assert np.array_equal(img, ref), int((img != ref).sum())
+    assert st["ray_steps"] == rst["ray_steps"] and st["endgame_evals"] == rst.get("endgame_evals", 0)
+
+
 def test_endgame_off_for_fp32_normals(chrome):
     """Bit 15 (fp32 normals) marches in pure 16-bit (no fp32x3 pass), on both schedules."""
     with nr.Renderer(0) as r:
