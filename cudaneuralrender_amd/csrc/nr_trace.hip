@@ -365,6 +365,12 @@ __global__ __launch_bounds__(EG && EGL ? 64 * NR_EG_WAVES : 256, EG ? NR_TRACE_B
             const TraceKargs *K = fresh_kargs();
             const RenderArgs &A = K->A;
             const TraceArgs &T = K->T;
+            // (and the queue constants derived from them, formed here instead of held)
+            const uint32_t QCHUNK = TWO ? (BATCH && T.nframes >= 4 ? NR_QUEUE_CHUNK_DENSE : NR_QUEUE_CHUNK_DENSE1) : NR_QUEUE_CHUNK;
+            const uint32_t QLOW = TWO ? QCHUNK : NR_QUEUE_LOW;
+            const long nchunks = T.nblocks;
+            const auto rq = __builtin_amdgcn_make_buffer_rsrc(T.pix_ctr, 0, 128 << T.nq_shift, 0x00020000);
+            const int nq = 1 << T.nq_shift;
 #endif
             // rays live in lanes [0, take): a wave capped at 16 or 32 rays marches 1 or
             // 2 tiles per iteration (short iterations when a frame shard is small)
