@@ -178,9 +178,12 @@ def test_endgame_deep_networks(chrome, extra):
         r.load_mlp(dims, K, B).set_precision("bf16")
         r.set_view(iv, nm, 0).set_static(nr.NR_COLOR_MATCAP, 3).set_scene("v1").set_matcap(chrome)
         img, st = r.render(112, 96, 96)
+        # a batch of the same frame twice (the batched instance of the same form)
+        imgs, bst = r.render_batch(112, 96, [(iv, nm, 0)] * 2, 96)
     ref, rst = net.render(112, 96, iv, nm, color_type=1, matcap=chrome, max_steps=96, nthreads=16, precision=1,
                           endgame=nr.NR_ENDGAME_DEFAULT)
     _check(img, st, ref, rst)
+    assert all(np.array_equal(x, ref) for x in imgs) and bst["endgame_evals"] == 2 * rst["endgame_evals"]
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
